@@ -1,0 +1,125 @@
+/*
+ * tcsc_oracle.h -- CPU restatement of the reference's TCSC hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (the HIP library under
+ * ternary-spgemm_amd/, the C-ABI in include/) links, loads or calls this code.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it,
+ * and only as the checker / the timed CPU baseline.
+ *
+ * Every function cites the reference file:line it restates
+ * (paths relative to alessiomelone/Ternary-spGEMM @ 2025-06-29).
+ *
+ * Pinning: the restatement is checked in tests/test_oracle.py against
+ *   - the reference's own TCSC constructor and dense GEMM / GEMM_PreLU oracle,
+ *     compiled unmodified from cpp_impl/data_structures/TCSC.h and
+ *     cpp_impl/sparseUtils.h into oracle/_ref/ (see oracle/Makefile), through
+ *     golden vectors committed under tests/golden/ (tests/golden/make_golden.py);
+ *   - the hand-worked 4x4 TCSC / BlockedTCSC<2> arrays in
+ *     plots/data_example_image/base_structure.py:19-30 and blocked.py:19-30.
+ * The kernel body of BaseTCSC itself (cpp_impl/comp.h:25-69) cannot be compiled
+ * here: comp.h includes <arm_neon.h> unconditionally (comp.h:6), which the x86
+ * image lacks.  Its accumulation ORDER for non-integer X is therefore pinned by
+ * this restatement of comp.h:37-63 alone (see DESIGN.md "Oracle").
+ */
+#ifndef TCSC_ORACLE_H
+#define TCSC_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- deterministic inputs ------------------------------------------------ */
+
+/* splitmix64 stream.  The reference uses std::mt19937 + uniform_int_distribution
+ * (sparseUtils.h:8-22,52-56) whose mapping is libstdc++-specific; we keep the
+ * reference's DISTRIBUTION with a portable generator. */
+uint64_t oracle_splitmix64(uint64_t *state);
+uint64_t oracle_below(uint64_t *state, uint64_t n); /* unbiased U{0..n-1} */
+
+/* Ternary K x N row-major W with the distribution of generateSparseMatrix
+ * (sparseUtils.h:25-90, uniformDistribution=false branch :52-87): for every
+ * row k, v ~ U{0..floor(N/s/20)+1}; (N/s)/2+v entries +1 then (N/s)/2-v entries
+ * -1 at uniformly random empty columns (rejection sampling, as :66-86).
+ * Counts are clamped to [0, N] (the reference would loop forever there). */
+void oracle_gen_ternary(int K, int N, int s, uint64_t seed, int32_t *W);
+
+/* X[i] = U{-range..range} as float (initX, sparseUtils.h:6-23). */
+void oracle_init_x_int(int64_t len, int range, uint64_t seed, float *X);
+
+/* Non-integer X with wide exponent spread: every partial sum rounds, so any
+ * change of summation order changes the bits.  Not in the reference; used to
+ * pin the accumulation order. */
+void oracle_init_x_frac(int64_t len, uint64_t seed, float *X);
+
+/* ---- TCSC format ----------------------------------------------------------- */
+
+/* Counts nonzeros of a dense ternary W (for sizing the encode buffers). */
+void oracle_tcsc_count(const int32_t *W, int K, int N, int64_t *nnz_pos, int64_t *nnz_neg);
+
+/* class TCSC ctor (TCSC.h:13-41): column-major walk, per column the k of every
+ * +1 (resp. -1) in ascending order; col_start_* has N+1 entries. */
+void oracle_tcsc_encode(const int32_t *W, int K, int N,
+                        int32_t *col_start_pos, int32_t *col_start_neg,
+                        int32_t *row_index_pos, int32_t *row_index_neg);
+
+/* TCSC.h:43-49: 4 * (2(N+1) + nnz). */
+int64_t oracle_tcsc_size_bytes(int N, int64_t nnz_pos, int64_t nnz_neg);
+
+/* DataStructureInterface::getVectorRepresentation (DataStructureInterface.hpp:13)
+ * for TCSC: back to a dense K x N row-major ternary matrix. */
+void oracle_tcsc_decode(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                        const int32_t *row_index_pos, const int32_t *row_index_neg,
+                        int K, int N, int32_t *W);
+
+/* BlockedTCSC<B> ctor (BlockedTCSC.h:15-41): col_start indexed [kblock*N + n],
+ * (K/B)*N + 1 entries each; K must be a multiple of B. */
+void oracle_blocked_tcsc_count(const int32_t *W, int K, int N, int B,
+                               int64_t *nnz_pos, int64_t *nnz_neg);
+void oracle_blocked_tcsc_encode(const int32_t *W, int K, int N, int B,
+                                int32_t *col_start_pos, int32_t *col_start_neg,
+                                int32_t *row_index_pos, int32_t *row_index_neg);
+
+/* ---- kernels ---------------------------------------------------------------- */
+
+/* BaseTCSC<float> (comp.h:25-69), same order: y=0; y+=X[m,k] over the +1 run
+ * ascending (:44-51); y-=X[m,k] over the -1 run ascending (:54-61);
+ * Y[m,n]=y+b[n] (:63).  Single thread, as the reference. */
+void oracle_base_tcsc(const float *X, const int32_t *col_start_pos, const int32_t *col_start_neg,
+                      const int32_t *row_index_pos, const int32_t *row_index_neg,
+                      const float *b, float *Y, int M, int N, int K);
+
+/* Same arithmetic, rows m split over OpenMP threads (our parallelisation; the
+ * reference is single-threaded).  Bit-identical to oracle_base_tcsc. */
+void oracle_base_tcsc_omp(const float *X, const int32_t *col_start_pos, const int32_t *col_start_neg,
+                          const int32_t *row_index_pos, const int32_t *row_index_neg,
+                          const float *b, float *Y, int M, int N, int K, int nthreads);
+
+/* DoubleUnrolledTCSC<float,4,4> (comp.h:1227-1438): the reference's fastest
+ * registered CPU kernel.  Different summation order from BaseTCSC; equal to it
+ * only for integer-valued X. */
+void oracle_double_unrolled_tcsc_k4m4(const float *X, const int32_t *col_start_pos,
+                                      const int32_t *col_start_neg, const int32_t *row_index_pos,
+                                      const int32_t *row_index_neg, const float *b, float *Y,
+                                      int M, int N, int K);
+
+/* BaseTCSC_PreLU<float> (comp_prelu.h:12-70): BaseTCSC, then
+ * Y = y > 0 ? y : alpha[n]*y (:57-67). */
+void oracle_base_tcsc_prelu(const float *X, const int32_t *col_start_pos, const int32_t *col_start_neg,
+                            const int32_t *row_index_pos, const int32_t *row_index_neg,
+                            const float *b, const float *alpha, float *Y, int M, int N, int K);
+
+/* BaseBlockedTCSC<float,B> (comp.h:607-658): per output, K-blocks in order,
+ * inside each block the +1 run then the -1 run.  (Order differs from BaseTCSC.) */
+void oracle_base_blocked_tcsc(const float *X, const int32_t *col_start_pos, const int32_t *col_start_neg,
+                              const int32_t *row_index_pos, const int32_t *row_index_neg,
+                              const float *b, float *Y, int M, int N, int K, int B);
+
+/* Dense GEMM oracle (sparseUtils.h:92-108): y=sum_k X[m,k]*W[k,n]; Y=y+b[n]. */
+void oracle_gemm_dense(const float *X, const float *W, const float *b, float *Y, int M, int N, int K);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
