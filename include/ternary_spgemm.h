@@ -1,0 +1,140 @@
+/*
+ * ternary_spgemm.h -- C-ABI of the MI355X-native ternary TCSC spGEMM.
+ *
+ *     Y[m,n] = ( sum_{k in P(n)} X[m,k]  -  sum_{k in N(n)} X[m,k] ) + b[n]
+ *
+ * with W in {-1,0,+1}^{K x N} given in the reference's TCSC layout
+ * (col_start_pos/neg: N+1 ints; row_index_pos/neg: ascending k per column).
+ * Results are bit-identical to the reference CPU kernel BaseTCSC<float>
+ * (cpp_impl/comp.h:25-69): every output is ONE serial fp32 chain
+ * 0 + x_p1 + ... + x_pP - x_n1 - ... - x_nQ, then + b[n].
+ *
+ * Plain pointers and sizes only; no torch or HIP types.  Every function
+ * returns TSG_OK (0) or a TSG_ERR_* code; tcsc_hip_last_error() gives text.
+ * Reference interfaces each entry point replaces are cited as
+ * path:line relative to alessiomelone/Ternary-spGEMM.
+ */
+#ifndef TERNARY_SPGEMM_H
+#define TERNARY_SPGEMM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSG_ABI_VERSION 1
+
+enum tsg_status {
+    TSG_OK = 0,
+    TSG_ERR_ARG = 1,     /* bad argument: null pointer, shape mismatch, malformed TCSC */
+    TSG_ERR_HIP = 2,     /* HIP runtime / launch failure */
+    TSG_ERR_NOMEM = 3,   /* device or host allocation failed */
+    TSG_ERR_NODEV = 4,   /* no usable gfx950 device */
+    TSG_ERR_RANGE = 5    /* size exceeds a supported limit */
+};
+
+/* Opaque handle: one TCSC weight matrix resident on one device (the device
+ * image built from the TCSC arrays at registration, plus a work buffer). */
+typedef struct tsg_tcsc tsg_tcsc;
+
+/* ---- registration ---------------------------------------------------------
+ * Replaces `std::make_shared<TCSC>(W_raw, K, N)` + capture in the
+ * add_function lambda (cpp_impl/main.cpp:63,76-81; TCSC.h:13-41): the format
+ * is built/uploaded ONCE, before any call.  Arrays are copied; the caller
+ * keeps ownership.  device < 0 selects the current HIP device.
+ * On failure *out is NULL and the status says why. */
+int tcsc_hip_create(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                    const int32_t *row_index_pos, const int32_t *row_index_neg,
+                    int K, int N, int device, tsg_tcsc **out);
+
+/* Same, from a dense row-major K x N ternary matrix (TCSC ctor semantics,
+ * TCSC.h:13-41; any value other than +1/-1 is treated as 0, as there). */
+int tcsc_hip_create_dense(const int32_t *W, int K, int N, int device, tsg_tcsc **out);
+
+/* Releases every device/host resource of the handle (NULL is a no-op). */
+void tcsc_hip_destroy(tsg_tcsc *h);
+
+/* ---- compute --------------------------------------------------------------
+ * Replaces one call of the registered comp_func
+ *   using comp_func = std::function<void(float*X, float*B, float*Y, int M, int N, int K)>
+ * (cpp_impl/common.h:12) bound to BaseTCSC<float> (comp.h:25-69).
+ * Argument order M, N, K as there.  HOST pointers: X is M x K row-major,
+ * b has N floats, Y is M x N row-major and is fully overwritten.
+ * Synchronous: Y is valid on return (main.cpp:214-216, perf.cpp:62-66). */
+int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K);
+
+/* DEVICE pointers (on the handle's device), enqueued on `stream`
+ * (a hipStream_t; NULL = legacy default stream); returns without waiting.
+ * The work buffer must be reserved for this M beforehand (tcsc_hip_reserve)
+ * for the call to be graph-capturable; otherwise it is grown on demand. */
+int tcsc_hip_gemm_dev(tsg_tcsc *h, const float *dX, const float *db, float *dY,
+                      int M, int N, int K, void *stream);
+
+/* PReLU twin: comp_func_prelu (common.h:13) bound to BaseTCSC_PreLU<float>
+ * (comp_prelu.h:12-70): y = chain + b[n]; Y = y > 0 ? y : alpha[n]*y. */
+int tcsc_hip_gemm_prelu(tsg_tcsc *h, const float *X, const float *b, const float *alpha,
+                        float *Y, int M, int N, int K);
+int tcsc_hip_gemm_prelu_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha,
+                            float *dY, int M, int N, int K, void *stream);
+
+/* Pre-allocates the per-handle work buffer for row counts up to max_M. */
+int tcsc_hip_reserve(tsg_tcsc *h, int max_M);
+
+/* ---- introspection ------------------------------------------------------- */
+typedef struct tsg_info {
+    int32_t K, N, device, abi_version;
+    int64_t nnz_pos, nnz_neg;
+    int64_t tcsc_bytes;     /* TCSC::getDataStructureSize() (TCSC.h:43-49) */
+    int64_t image_bytes;    /* bytes of the device image (segments + entries) */
+    int64_t work_bytes;     /* current work-buffer size */
+    int32_t chunk_rows;     /* K rows per LDS chunk of the device image */
+    int32_t tile_rows;      /* M rows per workgroup */
+    int32_t tile_cols;      /* N columns per workgroup */
+    int32_t reserved;
+} tsg_info;
+int tcsc_hip_info(const tsg_tcsc *h, tsg_info *out);
+
+/* DataStructureInterface::getVectorRepresentation (DataStructureInterface.hpp:13)
+ * for the registered matrix: dense K x N row-major ternary ints. */
+int tcsc_hip_to_dense(const tsg_tcsc *h, int32_t *W, int K, int N);
+
+/* Kernel timing: when enabled, HIP events bracket every launch of the main
+ * (dominant) kernel on its own stream; totals accumulate until reset. */
+int tcsc_hip_set_timing(tsg_tcsc *h, int enable);
+int tcsc_hip_kernel_time(tsg_tcsc *h, double *total_ms, int64_t *launches, int reset);
+
+const char *tcsc_hip_last_error(void);
+int tcsc_hip_device_count(int *count);
+
+/* ---- host-side helpers (no GPU needed) -------------------------------------
+ * Column slice [n0, n1) of a TCSC, rebased to start at 0: the shard a rank
+ * owns when W's columns are split across GPUs (Y[:,n] depends only on
+ * column n).  Pass NULL outputs to query nnz_pos/nnz_neg of the slice. */
+int tsg_tcsc_slice(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                   const int32_t *row_index_pos, const int32_t *row_index_neg, int N,
+                   int n0, int n1, int32_t *out_csp, int32_t *out_csn,
+                   int32_t *out_rip, int32_t *out_rin, int64_t *nnz_pos, int64_t *nnz_neg);
+
+/* Checks the TCSC invariants the kernels rely on: monotone col_start of
+ * length N+1 starting at 0, 0 <= k < K, strictly ascending k per column, no
+ * k both +1 and -1 in a column.  TSG_OK or TSG_ERR_ARG (with message). */
+int tsg_tcsc_validate(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                      const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N);
+
+/* Synthetic W with the distribution of generateSparseMatrix
+ * (cpp_impl/sparseUtils.h:52-87), emitted directly as TCSC restricted to the
+ * columns [n0, n1) (rebased).  Deterministic in `seed` (splitmix64 stream,
+ * the same draw sequence as the test oracle's dense generator).  Call with
+ * NULL arrays to get nnz_pos/nnz_neg, then again to fill. */
+int tsg_gen_tcsc(int K, int N, int s, uint64_t seed, int n0, int n1,
+                 int32_t *csp, int32_t *csn, int32_t *rip, int32_t *rin,
+                 int64_t *nnz_pos, int64_t *nnz_neg);
+
+/* X[i] = integer-valued fp32 U{-range..range} (initX, sparseUtils.h:6-23). */
+int tsg_gen_x(int64_t len, int range, uint64_t seed, float *X);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TERNARY_SPGEMM_H */

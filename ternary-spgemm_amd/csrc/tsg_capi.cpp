@@ -1,0 +1,394 @@
+// tsg_capi.cpp -- the C-ABI (include/ternary_spgemm.h): handle lifetime,
+// device image upload, work buffers, launches, host-pointer convenience path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ternary_spgemm.h"
+#include "tsg_internal.h"
+
+extern thread_local std::string g_tsg_host_err;  // one per-thread message for the whole ABI
+
+static int fail(int code, const std::string &msg)
+{
+    g_tsg_host_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(TSG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));  \
+    } while (0)
+
+struct tsg_tcsc {
+    int K = 0, N = 0, device = 0;
+    int64_t nnz_pos = 0, nnz_neg = 0;
+    tsg::Image img;                       // host copy of the device image
+    std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
+    uint32_t *d_seg = nullptr, *d_ent = nullptr;
+    float *d_work = nullptr;              // X^T [Kp][Mp]
+    size_t work_bytes = 0;
+    // host-pointer path staging (tcsc_hip_gemm): grow-only
+    float *d_x = nullptr, *d_b = nullptr, *d_y = nullptr, *d_alpha = nullptr;
+    size_t x_bytes = 0, y_bytes = 0;
+    hipStream_t stream = nullptr;         // stream of the host-pointer path
+    // timing of the main kernel
+    bool timing = false;
+    static constexpr int kRing = 256;     // event pairs in flight before a harvest blocks
+    hipEvent_t ev0[kRing] = {}, ev1[kRing] = {};
+    int ring_head = 0, ring_count = 0;    // pending pairs: [head - count, head)
+    double total_ms = 0.0;
+    int64_t launches = 0;
+    std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int check_device(int dev)
+{
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return fail(TSG_ERR_NODEV, "hipGetDeviceProperties failed for device " + std::to_string(dev));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(TSG_ERR_NODEV, std::string("device is ") + prop.gcnArchName +
+                                       "; this library is built for gfx950 (MI355X) only");
+    return TSG_OK;
+}
+
+int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp)
+{
+    Mp = ((std::max(M, 1) + tsg::kTileM - 1) / tsg::kTileM) * tsg::kTileM;
+    Kp = h->img.nch * tsg::kChunkK;
+    return TSG_OK;
+}
+
+int ensure_work(tsg_tcsc *h, int M)
+{
+    int Mp, Kp;
+    dims_for(h, M, Mp, Kp);
+    const size_t need = (size_t)Mp * Kp * sizeof(float);
+    if (need <= h->work_bytes) return TSG_OK;
+    if (h->d_work) HIP_TRY(hipFree(h->d_work));
+    h->d_work = nullptr;
+    h->work_bytes = 0;
+    if (hipMalloc(&h->d_work, need) != hipSuccess)
+        return fail(TSG_ERR_NOMEM, "hipMalloc of " + std::to_string(need) + " B work buffer failed");
+    h->work_bytes = need;
+    return TSG_OK;
+}
+
+// Folds finished event pairs into the totals.  `all` waits for every pending
+// pair; otherwise only the oldest is waited for (ring full).
+int harvest_timing(tsg_tcsc *h, bool all)
+{
+    int todo = all ? h->ring_count : (h->ring_count == tsg_tcsc::kRing ? 1 : 0);
+    while (todo-- > 0) {
+        const int i = (h->ring_head - h->ring_count + tsg_tcsc::kRing) % tsg_tcsc::kRing;
+        HIP_TRY(hipEventSynchronize(h->ev1[i]));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, h->ev0[i], h->ev1[i]));
+        h->total_ms += ms;
+        h->launches += 1;
+        h->ring_count--;
+    }
+    return TSG_OK;
+}
+
+int ensure_events(tsg_tcsc *h)
+{
+    if (h->ev0[0]) return TSG_OK;
+    for (int i = 0; i < tsg_tcsc::kRing; i++) {
+        HIP_TRY(hipEventCreate(&h->ev0[i]));
+        HIP_TRY(hipEventCreate(&h->ev1[i]));
+    }
+    return TSG_OK;
+}
+
+int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, float *dY, int M,
+            int N, int K, hipStream_t s, bool prelu)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    if (N != h->N || K != h->K)
+        return fail(TSG_ERR_ARG, "shape mismatch: handle has K=" + std::to_string(h->K) + " N=" +
+                                     std::to_string(h->N) + ", call has K=" + std::to_string(K) +
+                                     " N=" + std::to_string(N));
+    if (M < 0) return fail(TSG_ERR_ARG, "M < 0");
+    if (M == 0 || N == 0) return TSG_OK;
+    if (!dY || !db || (K > 0 && !dX) || (prelu && !dalpha))
+        return fail(TSG_ERR_ARG, "null device pointer");
+    DeviceGuard g(h->device);
+    int rc = ensure_work(h, M);
+    if (rc) return rc;
+    int Mp, Kp;
+    dims_for(h, M, Mp, Kp);
+    if (K == 0) {
+        // no X at all: chain is +0; X^T stays zero
+        HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
+    } else if (tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s) != 0) {
+        return fail(TSG_ERR_HIP, std::string("transpose launch: ") + hipGetErrorString(hipGetLastError()));
+    }
+    std::lock_guard<std::mutex> lk(h->mu);
+    int slot = -1;
+    if (h->timing) {
+        rc = harvest_timing(h, false);
+        if (rc) return rc;
+        slot = h->ring_head;
+        HIP_TRY(hipEventRecord(h->ev0[slot], s));
+    }
+    if (tsg::launch_tcsc(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->img.Npad,
+                         h->img.nch, h->img.tile_cols, prelu ? 1 : 0, s) != 0)
+        return fail(TSG_ERR_HIP, std::string("tcsc launch: ") + hipGetErrorString(hipGetLastError()));
+    if (slot >= 0) {
+        HIP_TRY(hipEventRecord(h->ev1[slot], s));
+        h->ring_head = (h->ring_head + 1) % tsg_tcsc::kRing;
+        h->ring_count++;
+    }
+    return TSG_OK;
+}
+
+int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, float *Y, int M,
+             int N, int K, bool prelu)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    if (N != h->N || K != h->K) return run_dev(h, nullptr, nullptr, nullptr, nullptr, M, N, K, nullptr, prelu);
+    if (M < 0) return fail(TSG_ERR_ARG, "M < 0");
+    if (M == 0 || N == 0) return TSG_OK;
+    if (!Y || !b || (K > 0 && !X) || (prelu && !alpha)) return fail(TSG_ERR_ARG, "null host pointer");
+    DeviceGuard g(h->device);
+    const size_t xb = (size_t)M * K * sizeof(float), yb = (size_t)M * N * sizeof(float);
+    if (xb > h->x_bytes) {
+        if (h->d_x) HIP_TRY(hipFree(h->d_x));
+        h->d_x = nullptr;
+        h->x_bytes = 0;
+        if (hipMalloc(&h->d_x, std::max<size_t>(xb, 4)) != hipSuccess) return fail(TSG_ERR_NOMEM, "hipMalloc X");
+        h->x_bytes = xb;
+    }
+    if (yb > h->y_bytes) {
+        if (h->d_y) HIP_TRY(hipFree(h->d_y));
+        h->d_y = nullptr;
+        h->y_bytes = 0;
+        if (hipMalloc(&h->d_y, yb) != hipSuccess) return fail(TSG_ERR_NOMEM, "hipMalloc Y");
+        h->y_bytes = yb;
+    }
+    if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    hipStream_t s = h->stream;
+    if (xb) HIP_TRY(hipMemcpyAsync(h->d_x, X, xb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(h->d_b, b, (size_t)N * sizeof(float), hipMemcpyHostToDevice, s));
+    if (prelu) HIP_TRY(hipMemcpyAsync(h->d_alpha, alpha, (size_t)N * sizeof(float), hipMemcpyHostToDevice, s));
+    int rc = run_dev(h, h->d_x, h->d_b, h->d_alpha, h->d_y, M, N, K, s, prelu);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(Y, h->d_y, yb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return TSG_OK;
+}
+
+void free_handle(tsg_tcsc *h)
+{
+    if (!h) return;
+    DeviceGuard g(h->device);
+    if (h->ring_count) (void)hipDeviceSynchronize();
+    for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_x,
+                    (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha})
+        if (p) (void)hipFree(p);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    for (int i = 0; i < tsg_tcsc::kRing; i++) {
+        if (h->ev0[i]) (void)hipEventDestroy(h->ev0[i]);
+        if (h->ev1[i]) (void)hipEventDestroy(h->ev1[i]);
+    }
+    delete h;
+}
+
+}  // namespace
+
+// ================================================================ C-ABI ==
+
+extern "C" const char *tcsc_hip_last_error(void)
+{
+    return g_tsg_host_err.c_str();
+}
+
+extern "C" int tcsc_hip_device_count(int *count)
+{
+    if (!count) return fail(TSG_ERR_ARG, "null count");
+    *count = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return fail(TSG_ERR_NODEV, "hipGetDeviceCount failed");
+    *count = n;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                               const int32_t *rin, int K, int N, int device, tsg_tcsc **out)
+{
+    if (!out) return fail(TSG_ERR_ARG, "null out");
+    *out = nullptr;
+    std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N);
+    if (!e.empty()) return fail(TSG_ERR_ARG, "malformed TCSC: " + e);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TSG_ERR_NODEV, "no HIP device");
+    if (device < 0) HIP_TRY(hipGetDevice(&device));
+    if (device >= ndev) return fail(TSG_ERR_ARG, "device index out of range");
+    int rc = check_device(device);
+    if (rc) return rc;
+
+    tsg_tcsc *h = new tsg_tcsc();
+    h->K = K;
+    h->N = N;
+    h->device = device;
+    h->nnz_pos = csp[N];
+    h->nnz_neg = csn[N];
+    h->csp.assign(csp, csp + N + 1);
+    h->csn.assign(csn, csn + N + 1);
+    if (h->nnz_pos) h->rip.assign(rip, rip + h->nnz_pos);
+    if (h->nnz_neg) h->rin.assign(rin, rin + h->nnz_neg);
+    tsg::build_image(csp, csn, rip, rin, K, N, tsg::pick_tile_cols(N), h->img);
+
+    DeviceGuard g(device);
+    const size_t sb = h->img.seg.size() * sizeof(uint32_t), eb = h->img.ent.size() * sizeof(uint32_t);
+    if (hipMalloc(&h->d_seg, sb) != hipSuccess || hipMalloc(&h->d_ent, eb) != hipSuccess ||
+        hipMalloc(&h->d_b, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
+        hipMalloc(&h->d_alpha, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess) {
+        free_handle(h);
+        return fail(TSG_ERR_NOMEM, "hipMalloc of the device image failed");
+    }
+    if (hipMemcpy(h->d_seg, h->img.seg.data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->d_ent, h->img.ent.data(), eb, hipMemcpyHostToDevice) != hipSuccess) {
+        free_handle(h);
+        return fail(TSG_ERR_HIP, "upload of the device image failed");
+    }
+    *out = h;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_create_dense(const int32_t *W, int K, int N, int device, tsg_tcsc **out)
+{
+    if (!out) return fail(TSG_ERR_ARG, "null out");
+    *out = nullptr;
+    if (!W || K < 0 || N < 0) return fail(TSG_ERR_ARG, "bad dense matrix");
+    // TCSC ctor (TCSC.h:13-41): column by column, +1 / -1 rows ascending
+    std::vector<int32_t> csp, csn, rip, rin;
+    csp.reserve((size_t)N + 1);
+    csn.reserve((size_t)N + 1);
+    for (int n = 0; n < N; n++) {
+        csp.push_back((int32_t)rip.size());
+        csn.push_back((int32_t)rin.size());
+        for (int k = 0; k < K; k++) {
+            const int32_t v = W[(size_t)k * N + n];
+            if (v == 1) rip.push_back(k);
+            else if (v == -1) rin.push_back(k);
+        }
+    }
+    csp.push_back((int32_t)rip.size());
+    csn.push_back((int32_t)rin.size());
+    return tcsc_hip_create(csp.data(), csn.data(), rip.data(), rin.data(), K, N, device, out);
+}
+
+extern "C" void tcsc_hip_destroy(tsg_tcsc *h) { free_handle(h); }
+
+extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
+{
+    if (!h || max_M < 0) return fail(TSG_ERR_ARG, "bad reserve arguments");
+    DeviceGuard g(h->device);
+    return ensure_work(h, max_M);
+}
+
+extern "C" int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K)
+{
+    return run_host(h, X, b, nullptr, Y, M, N, K, false);
+}
+
+extern "C" int tcsc_hip_gemm_prelu(tsg_tcsc *h, const float *X, const float *b, const float *alpha,
+                                   float *Y, int M, int N, int K)
+{
+    return run_host(h, X, b, alpha, Y, M, N, K, true);
+}
+
+extern "C" int tcsc_hip_gemm_dev(tsg_tcsc *h, const float *dX, const float *db, float *dY, int M,
+                                 int N, int K, void *stream)
+{
+    return run_dev(h, dX, db, nullptr, dY, M, N, K, (hipStream_t)stream, false);
+}
+
+extern "C" int tcsc_hip_gemm_prelu_dev(tsg_tcsc *h, const float *dX, const float *db,
+                                       const float *dalpha, float *dY, int M, int N, int K,
+                                       void *stream)
+{
+    return run_dev(h, dX, db, dalpha, dY, M, N, K, (hipStream_t)stream, true);
+}
+
+extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
+{
+    if (!h || !o) return fail(TSG_ERR_ARG, "null argument");
+    std::memset(o, 0, sizeof(*o));
+    o->K = h->K;
+    o->N = h->N;
+    o->device = h->device;
+    o->abi_version = TSG_ABI_VERSION;
+    o->nnz_pos = h->nnz_pos;
+    o->nnz_neg = h->nnz_neg;
+    o->tcsc_bytes = 4 * (2 * ((int64_t)h->N + 1) + h->nnz_pos + h->nnz_neg);
+    o->image_bytes = (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;
+    o->work_bytes = (int64_t)h->work_bytes;
+    o->chunk_rows = tsg::kChunkK;
+    o->tile_rows = tsg::kTileM;
+    o->tile_cols = h->img.tile_cols;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_to_dense(const tsg_tcsc *h, int32_t *W, int K, int N)
+{
+    if (!h || !W || K != h->K || N != h->N) return fail(TSG_ERR_ARG, "bad to_dense arguments");
+    std::memset(W, 0, sizeof(int32_t) * (size_t)K * N);
+    for (int n = 0; n < N; n++) {
+        for (int32_t i = h->csp[n]; i < h->csp[n + 1]; i++) W[(size_t)h->rip[i] * N + n] = 1;
+        for (int32_t i = h->csn[n]; i < h->csn[n + 1]; i++) W[(size_t)h->rin[i] * N + n] = -1;
+    }
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_set_timing(tsg_tcsc *h, int enable)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    int rc = enable ? ensure_events(h) : harvest_timing(h, true);
+    if (rc) return rc;
+    h->timing = enable != 0;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_kernel_time(tsg_tcsc *h, double *total_ms, int64_t *launches, int reset)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    int rc = harvest_timing(h, true);
+    if (rc) return rc;
+    if (total_ms) *total_ms = h->total_ms;
+    if (launches) *launches = h->launches;
+    if (reset) {
+        h->total_ms = 0.0;
+        h->launches = 0;
+    }
+    return TSG_OK;
+}

@@ -1,0 +1,242 @@
+// tsg_host.cpp -- host-side pieces of the product library that need no GPU:
+// the device-image planner, TCSC validation / column slicing for sharding,
+// and the synthetic-input generators used by bench.py and the driver.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ternary_spgemm.h"
+#include "tsg_internal.h"
+
+namespace tsg {
+
+int pick_tile_cols(int N)
+{
+    // kWaves waves x NW columns.  NW = 32 (64 accumulator VGPRs) unless N is
+    // so small that most of a 128-column tile would be padding.
+    return N <= 64 ? kWaves * 16 : kWaves * 32;
+}
+
+void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                 const int32_t *rin, int K, int N, int tile_cols, Image &img)
+{
+    img.K = K;
+    img.N = N;
+    img.tile_cols = tile_cols;
+    img.Npad = ((N + tile_cols - 1) / tile_cols) * tile_cols;
+    img.nch = std::max(1, (K + kChunkK - 1) / kChunkK);
+    const int nch = img.nch;
+    img.seg.assign((size_t)img.Npad * 2 * (nch + 1), 0u);
+    img.ent.clear();
+    const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
+    img.ent.reserve((size_t)(nnz / kEntPerWord) + (size_t)img.Npad * 2 * nch + 64);
+
+    for (int n = 0; n < img.Npad; n++) {
+        for (int p = 0; p < 2; p++) {
+            const int32_t *cs = p ? csn : csp;
+            const int32_t *ri = p ? rin : rip;
+            int32_t i = n < N ? cs[n] : 0;
+            const int32_t e = n < N ? cs[n + 1] : 0;
+            uint32_t *seg = &img.seg[((size_t)n * 2 + p) * (nch + 1)];
+            for (int j = 0; j < nch; j++) {
+                seg[j] = (uint32_t)img.ent.size();
+                const int32_t khi = (j + 1) * kChunkK;
+                uint32_t word = 0;
+                int fill = 0;
+                while (i < e && ri[i] < khi) {
+                    word |= (uint32_t)(ri[i] - j * kChunkK) << (8 * fill);
+                    if (++fill == kEntPerWord) {
+                        img.ent.push_back(word);
+                        word = 0;
+                        fill = 0;
+                    }
+                    i++;
+                }
+                if (fill) {  // pad the last group with the +0.0f row
+                    for (; fill < kEntPerWord; fill++) word |= (uint32_t)kZeroRow << (8 * fill);
+                    img.ent.push_back(word);
+                }
+            }
+            seg[nch] = (uint32_t)img.ent.size();
+        }
+    }
+    img.ent.resize(img.ent.size() + 64, 0u);  // tail: keeps any over-fetch in bounds
+}
+
+std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                          const int32_t *rin, int K, int N)
+{
+    if (K < 0 || N < 0) return "negative K or N";
+    if (!csp || !csn) return "null col_start array";
+    if (csp[0] != 0 || csn[0] != 0) return "col_start[0] must be 0";
+    for (int n = 0; n < N; n++) {
+        if (csp[n + 1] < csp[n]) return "col_start_pos not monotone at n=" + std::to_string(n);
+        if (csn[n + 1] < csn[n]) return "col_start_neg not monotone at n=" + std::to_string(n);
+    }
+    if ((csp[N] > 0 && !rip) || (csn[N] > 0 && !rin)) return "null row_index array";
+    for (int n = 0; n < N; n++) {
+        for (int p = 0; p < 2; p++) {
+            const int32_t *cs = p ? csn : csp;
+            const int32_t *ri = p ? rin : rip;
+            for (int32_t i = cs[n]; i < cs[n + 1]; i++) {
+                if (ri[i] < 0 || ri[i] >= K)
+                    return "row index out of [0,K) in column " + std::to_string(n);
+                if (i > cs[n] && ri[i] <= ri[i - 1])
+                    return "row indices not strictly ascending in column " + std::to_string(n);
+            }
+        }
+        // a k may not be both +1 and -1 in one column (the format encodes a
+        // single ternary value per (k, n))
+        int32_t a = csp[n], b = csn[n];
+        while (a < csp[n + 1] && b < csn[n + 1]) {
+            if (rip[a] == rin[b]) return "row index in both +1 and -1 runs of column " + std::to_string(n);
+            if (rip[a] < rin[b]) a++; else b++;
+        }
+    }
+    return std::string();
+}
+
+// splitmix64 + unbiased bounded draw: the same stream as the test oracle's
+// oracle_gen_ternary, so a seed names one W everywhere.
+static inline uint64_t splitmix64(uint64_t &s)
+{
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline uint64_t below(uint64_t &s, uint64_t n)
+{
+    if (n <= 1) return 0;
+    const uint64_t thresh = (0 - n) % n;
+    uint64_t x;
+    do x = splitmix64(s); while (x < thresh);
+    return x % n;
+}
+
+}  // namespace tsg
+
+// ---------------------------------------------------------------- C-ABI --
+
+thread_local std::string g_tsg_host_err;
+
+extern "C" int tsg_tcsc_validate(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                                 const int32_t *rin, int K, int N)
+{
+    std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N);
+    if (!e.empty()) {
+        g_tsg_host_err = e;
+        return TSG_ERR_ARG;
+    }
+    return TSG_OK;
+}
+
+extern "C" int tsg_tcsc_slice(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                              const int32_t *rin, int N, int n0, int n1, int32_t *ocsp,
+                              int32_t *ocsn, int32_t *orip, int32_t *orin, int64_t *nnz_pos,
+                              int64_t *nnz_neg)
+{
+    if (!csp || !csn || n0 < 0 || n1 < n0 || n1 > N) {
+        g_tsg_host_err = "tsg_tcsc_slice: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    const int32_t p0 = csp[n0], p1 = csp[n1], q0 = csn[n0], q1 = csn[n1];
+    if (nnz_pos) *nnz_pos = p1 - p0;
+    if (nnz_neg) *nnz_neg = q1 - q0;
+    if (ocsp)
+        for (int i = 0; i <= n1 - n0; i++) ocsp[i] = csp[n0 + i] - p0;
+    if (ocsn)
+        for (int i = 0; i <= n1 - n0; i++) ocsn[i] = csn[n0 + i] - q0;
+    if (orip && p1 > p0) std::memcpy(orip, rip + p0, sizeof(int32_t) * (size_t)(p1 - p0));
+    if (orin && q1 > q0) std::memcpy(orin, rin + q0, sizeof(int32_t) * (size_t)(q1 - q0));
+    return TSG_OK;
+}
+
+// generateSparseMatrix distribution (cpp_impl/sparseUtils.h:52-87), emitted
+// as TCSC of the columns [n0, n1).  Row k is drawn exactly as the oracle's
+// dense generator draws it; only entries of the slice are kept.
+extern "C" int tsg_gen_tcsc(int K, int N, int s, uint64_t seed, int n0, int n1, int32_t *csp,
+                            int32_t *csn, int32_t *rip, int32_t *rin, int64_t *nnz_pos,
+                            int64_t *nnz_neg)
+{
+    if (K < 0 || N < 0 || s <= 0 || n0 < 0 || n1 < n0 || n1 > N) {
+        g_tsg_host_err = "tsg_gen_tcsc: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    const int W = n1 - n0;
+    const int per_row = N / s, half = per_row / 2, vari = per_row / 20 + 1;
+    std::vector<int8_t> occ((size_t)N, 0);
+    std::vector<int32_t> touched;
+    touched.reserve((size_t)per_row + 8);
+    // row-major shard: (k, col, sign) in row order; per column counts
+    std::vector<int64_t> cntp((size_t)W + 1, 0), cntn((size_t)W + 1, 0);
+    std::vector<int32_t> rowcol;   // packed (col - n0) for kept entries, row order
+    std::vector<int8_t> rowsgn;
+    std::vector<int32_t> rowk;
+    const bool fill = csp && csn;
+    uint64_t st = seed;
+    for (int k = 0; k < K; k++) {
+        const int v = (int)tsg::below(st, (uint64_t)vari + 1);
+        int npos = half + v, nneg = half - v;
+        if (npos > N) npos = N;
+        if (nneg < 0) nneg = 0;
+        if (nneg > N - npos) nneg = N - npos;
+        touched.clear();
+        for (int c = 0; c < npos;) {
+            const int col = (int)tsg::below(st, (uint64_t)N);
+            if (occ[col] == 0) { occ[col] = 1; touched.push_back(col); c++; }
+        }
+        for (int c = 0; c < nneg;) {
+            const int col = (int)tsg::below(st, (uint64_t)N);
+            if (occ[col] == 0) { occ[col] = -1; touched.push_back(col); c++; }
+        }
+        for (int32_t col : touched) {
+            if (col >= n0 && col < n1) {
+                if (occ[col] > 0) cntp[col - n0 + 1]++; else cntn[col - n0 + 1]++;
+                if (fill) {
+                    rowk.push_back(k);
+                    rowcol.push_back(col - n0);
+                    rowsgn.push_back(occ[col]);
+                }
+            }
+            occ[col] = 0;
+        }
+    }
+    for (int i = 0; i < W; i++) {
+        cntp[i + 1] += cntp[i];
+        cntn[i + 1] += cntn[i];
+    }
+    if (nnz_pos) *nnz_pos = cntp[W];
+    if (nnz_neg) *nnz_neg = cntn[W];
+    if (cntp[W] > INT32_MAX || cntn[W] > INT32_MAX) {
+        g_tsg_host_err = "tsg_gen_tcsc: slice nnz exceeds int32 (shard the columns)";
+        return TSG_ERR_RANGE;
+    }
+    if (!fill) return TSG_OK;
+    for (int i = 0; i <= W; i++) {
+        csp[i] = (int32_t)cntp[i];
+        csn[i] = (int32_t)cntn[i];
+    }
+    // counting sort by column; rows arrive in ascending k so each column's
+    // list is ascending, as TCSC.h:23-36 produces it
+    std::vector<int64_t> curp(cntp.begin(), cntp.end() - 1), curn(cntn.begin(), cntn.end() - 1);
+    for (size_t e = 0; e < rowk.size(); e++) {
+        const int c = rowcol[e];
+        if (rowsgn[e] > 0) rip[curp[c]++] = rowk[e];
+        else rin[curn[c]++] = rowk[e];
+    }
+    return TSG_OK;
+}
+
+extern "C" int tsg_gen_x(int64_t len, int range, uint64_t seed, float *X)
+{
+    if (len < 0 || range < 0 || (len > 0 && !X)) {
+        g_tsg_host_err = "tsg_gen_x: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    uint64_t st = seed;
+    for (int64_t i = 0; i < len; i++)
+        X[i] = (float)((int64_t)tsg::below(st, 2ull * (uint64_t)range + 1) - range);
+    return TSG_OK;
+}

@@ -1,0 +1,335 @@
+"""Python host mirror of the reference's plugin surface, over the C-ABI.
+
+The reference registers kernels as
+    using comp_func = std::function<void(float*X, float*B, float*Y, int M, int N, int K)>
+    add_function(comp_func f, std::string name)          (cpp_impl/common.h:12-15,
+                                                           cpp_impl/main.cpp:21-26)
+with a TCSC built once before registration (main.cpp:63,76-81).  This module
+keeps that shape for Python callers (tests, bench.py, the multi-GPU launcher):
+
+    h  = TCSCDevice(csp, csn, rip, rin, K, N)           # upload once
+    add_function(h.comp_func(), "HipBaseTCSC")          # registry, as main.cpp
+    h(X, B, Y, M, N, K)                                  # host pointers, sync
+
+plus device-pointer entry points for torch tensors.  Everything routes to
+libternary_spgemm.so (HIP, gfx950); there is no CPU fallback: if the library
+or a gfx950 device is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libternary_spgemm.so")
+
+TSG_OK = 0
+_ERRNAMES = {1: "TSG_ERR_ARG", 2: "TSG_ERR_HIP", 3: "TSG_ERR_NOMEM", 4: "TSG_ERR_NODEV",
+             5: "TSG_ERR_RANGE"}
+
+# Every symbol include/ternary_spgemm.h declares (tests check the .so exports them).
+EXPORTED_SYMBOLS = (
+    "tcsc_hip_create", "tcsc_hip_create_dense", "tcsc_hip_destroy", "tcsc_hip_gemm",
+    "tcsc_hip_gemm_dev", "tcsc_hip_gemm_prelu", "tcsc_hip_gemm_prelu_dev", "tcsc_hip_reserve",
+    "tcsc_hip_info", "tcsc_hip_to_dense", "tcsc_hip_set_timing", "tcsc_hip_kernel_time",
+    "tcsc_hip_last_error", "tcsc_hip_device_count", "tsg_tcsc_slice", "tsg_tcsc_validate",
+    "tsg_gen_tcsc", "tsg_gen_x",
+)
+
+
+class TSGError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where}: {_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class tsg_info(C.Structure):
+    _fields_ = [("K", C.c_int32), ("N", C.c_int32), ("device", C.c_int32),
+                ("abi_version", C.c_int32), ("nnz_pos", C.c_int64), ("nnz_neg", C.c_int64),
+                ("tcsc_bytes", C.c_int64), ("image_bytes", C.c_int64), ("work_bytes", C.c_int64),
+                ("chunk_rows", C.c_int32), ("tile_rows", C.c_int32), ("tile_cols", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+_LIB: Optional[C.CDLL] = None
+
+
+def build(jobs: int = 8) -> str:
+    """Compile the HIP library in-tree for gfx950 (hipcc cross-compiles; no GPU needed)."""
+    subprocess.run(["make", "-s", "-C", PKG_DIR, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    """Load libternary_spgemm.so.  torch (when installed) is imported first so
+    that the library binds to the same libamdhip64 runtime as torch."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    try:  # share one HIP runtime with torch (same soname libamdhip64.so.7)
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} missing: run __graft_entry__.build() or `make -C {PKG_DIR}`")
+    L = C.CDLL(LIB_PATH)
+    i32p, f32p, vp = C.POINTER(C.c_int32), C.POINTER(C.c_float), C.c_void_p
+    H = C.c_void_p
+    L.tcsc_hip_create.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.POINTER(H)]
+    L.tcsc_hip_create_dense.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(H)]
+    L.tcsc_hip_destroy.argtypes = [H]
+    L.tcsc_hip_destroy.restype = None
+    L.tcsc_hip_gemm.argtypes = [H, vp, vp, vp, C.c_int, C.c_int, C.c_int]
+    L.tcsc_hip_gemm_dev.argtypes = [H, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]
+    L.tcsc_hip_gemm_prelu.argtypes = [H, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int]
+    L.tcsc_hip_gemm_prelu_dev.argtypes = [H, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]
+    L.tcsc_hip_reserve.argtypes = [H, C.c_int]
+    L.tcsc_hip_info.argtypes = [H, C.POINTER(tsg_info)]
+    L.tcsc_hip_to_dense.argtypes = [H, vp, C.c_int, C.c_int]
+    L.tcsc_hip_set_timing.argtypes = [H, C.c_int]
+    L.tcsc_hip_kernel_time.argtypes = [H, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int]
+    L.tcsc_hip_last_error.argtypes = []
+    L.tcsc_hip_last_error.restype = C.c_char_p
+    L.tcsc_hip_device_count.argtypes = [C.POINTER(C.c_int)]
+    L.tsg_tcsc_slice.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp,
+                                 C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.tsg_tcsc_validate.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int]
+    L.tsg_gen_tcsc.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
+                               vp, vp, vp, vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.tsg_gen_x.argtypes = [C.c_int64, C.c_int, C.c_uint64, vp]
+    for f in EXPORTED_SYMBOLS:
+        if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error"):
+            getattr(L, f).restype = C.c_int
+    _LIB = L
+    return L
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != TSG_OK:
+        raise TSGError(rc, where, lib().tcsc_hip_last_error().decode(errors="replace"))
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None or a.size == 0 else a.ctypes.data
+
+
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+# ------------------------------------------------------------ host helpers --
+
+def validate(csp, csn, rip, rin, K: int, N: int) -> None:
+    """Raise TSGError(TSG_ERR_ARG) unless the arrays form a valid TCSC."""
+    csp, csn, rip, rin = map(_i32, (csp, csn, rip, rin))
+    _check(lib().tsg_tcsc_validate(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N),
+           "tsg_tcsc_validate")
+
+
+def tcsc_slice(csp, csn, rip, rin, N: int, n0: int, n1: int):
+    """Columns [n0, n1) of a TCSC, rebased (the per-rank shard)."""
+    csp, csn, rip, rin = map(_i32, (csp, csn, rip, rin))
+    p, q = C.c_int64(), C.c_int64()
+    L = lib()
+    _check(L.tsg_tcsc_slice(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), N, n0, n1,
+                            None, None, None, None, C.byref(p), C.byref(q)), "tsg_tcsc_slice")
+    o = [np.empty(n1 - n0 + 1, np.int32), np.empty(n1 - n0 + 1, np.int32),
+         np.empty(p.value, np.int32), np.empty(q.value, np.int32)]
+    _check(L.tsg_tcsc_slice(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), N, n0, n1,
+                            o[0].ctypes.data, o[1].ctypes.data, _ptr(o[2]), _ptr(o[3]),
+                            C.byref(p), C.byref(q)), "tsg_tcsc_slice")
+    return tuple(o)
+
+
+def gen_tcsc(K: int, N: int, s: int, seed: int, n0: int = 0, n1: Optional[int] = None):
+    """Synthetic TCSC (generateSparseMatrix distribution, sparseUtils.h:52-87) of
+    columns [n0, n1), rebased; deterministic in seed."""
+    n1 = N if n1 is None else n1
+    p, q = C.c_int64(), C.c_int64()
+    L = lib()
+    _check(L.tsg_gen_tcsc(K, N, s, seed, n0, n1, None, None, None, None, C.byref(p), C.byref(q)),
+           "tsg_gen_tcsc")
+    o = [np.empty(n1 - n0 + 1, np.int32), np.empty(n1 - n0 + 1, np.int32),
+         np.empty(max(p.value, 1), np.int32), np.empty(max(q.value, 1), np.int32)]
+    _check(L.tsg_gen_tcsc(K, N, s, seed, n0, n1, o[0].ctypes.data, o[1].ctypes.data,
+                          o[2].ctypes.data, o[3].ctypes.data, C.byref(p), C.byref(q)),
+           "tsg_gen_tcsc")
+    return o[0], o[1], o[2][: p.value], o[3][: q.value]
+
+
+def gen_x(M: int, K: int, seed: int, rng: int = 512) -> np.ndarray:
+    """Integer-valued fp32 X in [-rng, rng] (initX, sparseUtils.h:6-23)."""
+    X = np.empty((M, K), np.float32)
+    _check(lib().tsg_gen_x(M * K, rng, seed, _ptr(X)), "tsg_gen_x")
+    return X
+
+
+def device_count() -> int:
+    n = C.c_int()
+    _check(lib().tcsc_hip_device_count(C.byref(n)), "tcsc_hip_device_count")
+    return n.value
+
+
+# ------------------------------------------------------------------ handle --
+
+class TCSCDevice:
+    """One TCSC weight matrix resident on one GPU (tcsc_hip_create)."""
+
+    def __init__(self, csp, csn, rip, rin, K: int, N: int, device: int = -1):
+        csp, csn, rip, rin = map(_i32, (csp, csn, rip, rin))
+        self.K, self.N = int(K), int(N)
+        h = C.c_void_p()
+        _check(lib().tcsc_hip_create(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), self.K,
+                                     self.N, device, C.byref(h)), "tcsc_hip_create")
+        self._h = h
+
+    @classmethod
+    def from_dense(cls, W, device: int = -1) -> "TCSCDevice":
+        W = _i32(W)
+        K, N = W.shape
+        self = cls.__new__(cls)
+        self.K, self.N = int(K), int(N)
+        h = C.c_void_p()
+        _check(lib().tcsc_hip_create_dense(_ptr(W), K, N, device, C.byref(h)),
+               "tcsc_hip_create_dense")
+        self._h = h
+        return self
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().tcsc_hip_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- comp_func surface (host pointers, synchronous) ----
+    def __call__(self, X, B, Y, M: int, N: int, K: int) -> None:
+        """comp_func(X, B, Y, M, N, K) on numpy arrays (common.h:12)."""
+        assert X.dtype == np.float32 and B.dtype == np.float32 and Y.dtype == np.float32
+        assert X.flags.c_contiguous and Y.flags.c_contiguous and B.flags.c_contiguous
+        assert X.size >= M * K and B.size >= N and Y.size >= M * N
+        _check(lib().tcsc_hip_gemm(self._h, X.ctypes.data, B.ctypes.data, Y.ctypes.data, M, N, K),
+               "tcsc_hip_gemm")
+
+    def comp_func(self) -> Callable:
+        return lambda X, B, Y, M, N, K: self(X, B, Y, M, N, K)
+
+    def prelu(self, X, B, alpha, Y, M: int, N: int, K: int) -> None:
+        """comp_func_prelu(X, B, alpha, Y, M, N, K) (common.h:13)."""
+        _check(lib().tcsc_hip_gemm_prelu(self._h, X.ctypes.data, B.ctypes.data, alpha.ctypes.data,
+                                         Y.ctypes.data, M, N, K), "tcsc_hip_gemm_prelu")
+
+    def gemm(self, X, b) -> np.ndarray:
+        X, b = _f32(X), _f32(b)
+        M = X.shape[0]
+        Y = np.empty((M, self.N), np.float32)
+        self(X, b, Y, M, self.N, self.K)
+        return Y
+
+    def gemm_prelu(self, X, b, alpha) -> np.ndarray:
+        X, b, alpha = _f32(X), _f32(b), _f32(alpha)
+        M = X.shape[0]
+        Y = np.empty((M, self.N), np.float32)
+        self.prelu(X, b, alpha, Y, M, self.N, self.K)
+        return Y
+
+    # ---- device pointers (torch tensors), asynchronous on `stream` ----
+    def gemm_dev(self, dX: int, db: int, dY: int, M: int, stream: int = 0,
+                 dalpha: Optional[int] = None) -> None:
+        if dalpha is None:
+            _check(lib().tcsc_hip_gemm_dev(self._h, dX, db, dY, M, self.N, self.K, stream or None),
+                   "tcsc_hip_gemm_dev")
+        else:
+            _check(lib().tcsc_hip_gemm_prelu_dev(self._h, dX, db, dalpha, dY, M, self.N, self.K,
+                                                 stream or None), "tcsc_hip_gemm_prelu_dev")
+
+    def gemm_torch(self, X, b, Y=None, alpha=None):
+        """X [M,K] fp32 cuda tensor -> Y [M,N], enqueued on torch's current stream."""
+        import torch
+        assert X.is_cuda and X.dtype == torch.float32 and X.is_contiguous()
+        M = X.shape[0]
+        if Y is None:
+            Y = torch.empty((M, self.N), dtype=torch.float32, device=X.device)
+        stream = torch.cuda.current_stream(X.device).cuda_stream
+        self.gemm_dev(X.data_ptr(), b.data_ptr(), Y.data_ptr(), M, stream,
+                      None if alpha is None else alpha.data_ptr())
+        return Y
+
+    def reserve(self, max_M: int) -> None:
+        _check(lib().tcsc_hip_reserve(self._h, max_M), "tcsc_hip_reserve")
+
+    def info(self) -> dict:
+        o = tsg_info()
+        _check(lib().tcsc_hip_info(self._h, C.byref(o)), "tcsc_hip_info")
+        return {f: getattr(o, f) for f, _ in tsg_info._fields_}
+
+    def to_dense(self) -> np.ndarray:
+        """getVectorRepresentation (DataStructureInterface.hpp:13)."""
+        W = np.empty((self.K, self.N), np.int32)
+        _check(lib().tcsc_hip_to_dense(self._h, _ptr(W), self.K, self.N), "tcsc_hip_to_dense")
+        return W
+
+    def set_timing(self, on: bool) -> None:
+        _check(lib().tcsc_hip_set_timing(self._h, int(bool(on))), "tcsc_hip_set_timing")
+
+    def kernel_time(self, reset: bool = False) -> Tuple[float, int]:
+        ms, n = C.c_double(), C.c_int64()
+        _check(lib().tcsc_hip_kernel_time(self._h, C.byref(ms), C.byref(n), int(reset)),
+               "tcsc_hip_kernel_time")
+        return ms.value, n.value
+
+
+# ------------------------------------------------------- plugin registry --
+# Mirrors main.cpp:12-33: global lists of callables + names; "BaseTCSC" is the
+# speedup baseline name there (main.cpp:10).
+
+userFuncs: List[Callable] = []
+funcNames: List[str] = []
+userFuncs_prelu: List[Callable] = []
+funcNames_prelu: List[str] = []
+
+
+def add_function(f: Callable, name: str) -> None:
+    userFuncs.append(f)
+    funcNames.append(name)
+
+
+def add_prelu_function(f: Callable, name: str) -> None:
+    userFuncs_prelu.append(f)
+    funcNames_prelu.append(name)
+
+
+def clear_registry() -> None:
+    for lst in (userFuncs, funcNames, userFuncs_prelu, funcNames_prelu):
+        lst.clear()
+
+
+# --------------------------------------------------------------- metrics --
+
+def flops(M: int, N: int, nnz: int) -> int:
+    """Instrumented add/sub count of BaseTCSC (comp.h:28-31,48-50,63):
+    one per nonzero per row plus the bias add = M*(nnz + N) = M*N*(K/s+1)."""
+    return M * (nnz + N)
+
+
+def algorithmic_bytes(M: int, N: int, K: int, nnz: int) -> int:
+    """main.cpp:267 + TCSC.h:43-49: X, Y, b once, plus the TCSC arrays."""
+    return 4 * (M * K + M * N + N) + 4 * (2 * (N + 1) + nnz)

@@ -1,0 +1,191 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden
+vectors and the CPU oracle, bit for bit (integer AND non-integer X, so the
+accumulation order of BaseTCSC, cpp_impl/comp.h:37-63, is pinned).
+
+All cases call libternary_spgemm.so; nothing here falls back to the CPU.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _sha(*arrays) -> str:
+    return hashlib.sha256(np.concatenate([np.ascontiguousarray(a).ravel() for a in arrays]).tobytes()).hexdigest()
+
+
+def _bits_eq(a, b):
+    a, b = np.ascontiguousarray(a, np.float32), np.ascontiguousarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.fixture(scope="module")
+def small():
+    return np.load(os.path.join(GOLDEN, "ref_small.npz"))
+
+
+def _case_prefixes(z):
+    return sorted({k.split("_")[0] + "_" for k in z.files})
+
+
+def test_kat_4x4(tsg):
+    kat = json.load(open(os.path.join(GOLDEN, "kat_tcsc_4x4.json")))
+    h = tsg.TCSCDevice(kat["col_start_pos"], kat["col_start_neg"], kat["row_index_pos"],
+                       kat["row_index_neg"], 4, 4)
+    Y = h.gemm(np.array(kat["X"], np.float32), np.array(kat["b"], np.float32))
+    assert _bits_eq(Y, kat["Y_base_tcsc_oracle"])
+    assert np.array_equal(h.to_dense(), np.array(kat["W"]))
+
+
+def test_golden_small(tsg, small):
+    z = small
+    for p in _case_prefixes(z):
+        M, K, N, s, seed = (int(v) for v in z[p + "shape"])
+        pos = np.unpackbits(z[p + "Wpos_bits"])[: K * N].reshape(K, N).astype(np.int32)
+        neg = np.unpackbits(z[p + "Wneg_bits"])[: K * N].reshape(K, N).astype(np.int32)
+        W = pos - neg
+        if p + "csp" in z.files:
+            h = tsg.TCSCDevice(z[p + "csp"], z[p + "csn"], z[p + "rip"], z[p + "rin"], K, N)
+        else:
+            h = tsg.TCSCDevice.from_dense(W)
+        assert np.array_equal(h.to_dense(), W)
+        b, alpha = z[p + "b"], z[p + "alpha"]
+        assert _bits_eq(h.gemm(z[p + "X"], b), z[p + "Y_ref_gemm"]), p
+        assert _bits_eq(h.gemm(z[p + "Xfrac"], b), z[p + "Yfrac_oracle"]), p
+        assert _bits_eq(h.gemm_prelu(z[p + "X"], b, alpha), z[p + "Y_ref_gemm_prelu"]), p
+        assert _bits_eq(h.gemm_prelu(z[p + "Xfrac"], b, alpha), z[p + "Yfrac_prelu_oracle"]), p
+        h.close()
+
+
+EDGE = [
+    # (M, K, N, s): ragged tiles (128-row M tile, 128-col N tile, 128-row K chunk)
+    (1, 1, 1, 1), (1, 64, 96, 2), (2, 127, 3, 1), (127, 129, 63, 4), (128, 128, 64, 2),
+    (129, 257, 65, 4), (300, 1000, 129, 16), (64, 513, 1000, 8), (5, 4096, 17, 4),
+    (200, 96, 2048, 4),
+]
+
+
+@pytest.mark.parametrize("M,K,N,s", EDGE)
+def test_edges_vs_oracle(tsg, oracle_mod, M, K, N, s):
+    O = oracle_mod
+    W = O.gen_ternary(K, N, s, M * 7 + K)
+    t = O.tcsc_encode(W)
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
+    alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
+    for X in (O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)):
+        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+        assert _bits_eq(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
+
+
+def test_structural_edges(tsg, oracle_mod):
+    """All-zero W, fully dense ternary W, empty and full columns, K=0."""
+    O = oracle_mod
+    rng = np.random.default_rng(3)
+    for W in (np.zeros((300, 70), np.int32),
+              rng.integers(-1, 2, size=(260, 150)).astype(np.int32),
+              np.ones((129, 5), np.int32), -np.ones((129, 5), np.int32)):
+        K, N = W.shape
+        W[:, 0] = 0  # an empty column
+        t = O.tcsc_encode(W)
+        h = tsg.TCSCDevice(*t.arrays, K, N)
+        X = O.init_x_frac(131, K, 9)
+        b = rng.standard_normal(N).astype(np.float32)
+        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+    # K = 0: the chain is the +0.0 start, Y = 0 + b
+    h = tsg.TCSCDevice(np.zeros(4, np.int32), np.zeros(4, np.int32), [], [], 0, 3)
+    Y = h.gemm(np.zeros((5, 0), np.float32), np.array([1.5, -2.0, 0.0], np.float32))
+    assert _bits_eq(Y, np.tile(np.array([1.5, -2.0, 0.0], np.float32), (5, 1)))
+
+
+def test_config2_golden_hash(tsg):
+    """BASELINE.json configs[1]: M=512 K=4096 N=4096 s=4; Y hash from the
+    reference's dense GEMM (tests/golden/ref_hashes.json)."""
+    g = json.load(open(os.path.join(GOLDEN, "ref_hashes.json")))["config2"]
+    M, K, N, s = g["M"], g["K"], g["N"], g["s"]
+    arrs = tsg.gen_tcsc(K, N, s, g["seed_w"])
+    assert _sha(*arrs) == g["sha256_tcsc"]
+    h = tsg.TCSCDevice(*arrs, K, N)
+    X = tsg.gen_x(M, K, g["seed_x"])
+    Y = h.gemm(X, np.full(N, 2.0, np.float32))
+    assert Y[0, 0] == g["Y_0_0"] and Y[-1, -1] == g["Y_last"]
+    assert _sha(Y) == g["sha256_Y"]
+
+
+def test_config3_full_size(tsg, oracle_mod):
+    """BASELINE.json configs[2] at full size (M=4096 K=4096 N=16384 s=4):
+    sampled rows equal the reference GEMM (hash) for integer X, and the
+    oracle bit for bit for non-integer X (order at full size)."""
+    import torch
+    O = oracle_mod
+    g = json.load(open(os.path.join(GOLDEN, "ref_hashes.json")))["config3_rows"]
+    M, K, N, s = g["M"], g["K"], g["N"], g["s"]
+    arrs = tsg.gen_tcsc(K, N, s, g["seed_w"])
+    assert _sha(*arrs) == g["sha256_tcsc"]
+    h = tsg.TCSCDevice(*arrs, K, N)
+    rows = np.array(g["rows"])
+    b = np.full(N, 2.0, np.float32)
+    dev = torch.device("cuda:0")
+    bt = torch.from_numpy(b).to(dev)
+    X = torch.from_numpy(tsg.gen_x(M, K, g["seed_x"])).to(dev)
+    Y = h.gemm_torch(X, bt)
+    torch.cuda.synchronize()
+    assert _sha(Y[torch.from_numpy(rows).to(dev)].cpu().numpy()) == g["sha256_Y_rows"]
+    # non-integer X, order pinned against the oracle on sampled rows
+    Xf = O.init_x_frac(M, K, 77)
+    Yf = h.gemm_torch(torch.from_numpy(Xf).to(dev), bt).cpu().numpy()
+    t = O.TCSC(*arrs, K, N)
+    sub = rows[:8]
+    assert _bits_eq(Yf[sub], O.base_tcsc(np.ascontiguousarray(Xf[sub]), t, b))
+    # size-independent property: Y is fully overwritten (no stale values)
+    Y2 = torch.full((M, N), float("nan"), device=dev)
+    h.gemm_torch(X, bt, Y=Y2)
+    torch.cuda.synchronize()
+    assert torch.equal(Y2, Y)
+
+
+def test_device_path_streams_and_timing(tsg, oracle_mod):
+    import torch
+    O = oracle_mod
+    K, N, M = 700, 513, 333
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 1))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.reserve(M)
+    X = O.init_x_frac(M, K, 2)
+    b = np.linspace(-1, 1, N).astype(np.float32)
+    ref = O.base_tcsc(X, t, b)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        Xd, bd = torch.from_numpy(X).cuda(), torch.from_numpy(b).cuda()
+        h.set_timing(True)
+        for _ in range(3):
+            Y = h.gemm_torch(Xd, bd)
+    s.synchronize()
+    ms, n = h.kernel_time(reset=True)
+    assert n == 3 and ms > 0
+    assert _bits_eq(Y.cpu().numpy(), ref)
+    info = h.info()
+    assert info["K"] == K and info["N"] == N and info["nnz_pos"] == len(t.row_index_pos)
+    assert info["tcsc_bytes"] == t.size_bytes()
+
+
+def test_errors_are_loud(tsg, oracle_mod):
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(64, 32, 4, 1))
+    h = tsg.TCSCDevice(*t.arrays, 64, 32)
+    X = np.zeros((4, 64), np.float32)
+    Y = np.zeros((4, 32), np.float32)
+    b = np.zeros(32, np.float32)
+    with pytest.raises(tsg.TSGError) as e:
+        h(X, b, Y, 4, 31, 64)  # N mismatch
+    assert e.value.code == 1
+    with pytest.raises(tsg.TSGError):
+        tsg.TCSCDevice(t.col_start_pos, t.col_start_neg, t.row_index_pos[::-1].copy(),
+                       t.row_index_neg, 64, 32)
+    h(X, b, Y, 0, 32, 64)  # M = 0 is a no-op, as the reference's empty loop

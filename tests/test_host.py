@@ -1,0 +1,108 @@
+"""Host-side logic of the product library (no GPU needed): the C-ABI .so loads
+and exports every function include/ternary_spgemm.h declares, the TCSC
+validation / slicing / generators agree with the oracle, and GPU entry points
+fail loudly (no CPU fallback) when there is no device."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO, gpu_available
+
+
+def _declared_functions():
+    text = open(os.path.join(REPO, "include", "ternary_spgemm.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(t\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_symbols_exported(tsg):
+    declared = _declared_functions()
+    assert len(declared) >= 18
+    assert sorted(tsg.EXPORTED_SYMBOLS) == declared
+    L = ctypes.CDLL(tsg.LIB_PATH)
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+def test_library_is_gfx950_code(tsg):
+    """The .so carries a gfx950 code object (hipcc --offload-arch=gfx950)."""
+    blob = open(tsg.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_generator_matches_oracle(tsg, oracle_mod):
+    O = oracle_mod
+    for K, N, s, seed in [(64, 256, 4, 1), (100, 37, 2, 5), (33, 7, 16, 3), (512, 1024, 8, 77)]:
+        t = O.tcsc_encode(O.gen_ternary(K, N, s, seed))
+        g = tsg.gen_tcsc(K, N, s, seed)
+        for a, b in zip(t.arrays, g):
+            assert np.array_equal(a, b)
+        n0, n1 = N // 3, N // 2 + 1
+        sl = tsg.gen_tcsc(K, N, s, seed, n0, n1)
+        ref = tsg.tcsc_slice(*t.arrays, N, n0, n1)
+        for a, b in zip(sl, ref):
+            assert np.array_equal(a, b)
+        # slice == encoding of the dense column block
+        tb = O.tcsc_encode(t.dense()[:, n0:n1])
+        for a, b in zip(tb.arrays, ref):
+            assert np.array_equal(a, b)
+    X = tsg.gen_x(5, 7, 11)
+    assert np.array_equal(X, O.init_x_int(5, 7, 11))
+
+
+def test_slices_tile_the_matrix(tsg, oracle_mod):
+    O = oracle_mod
+    K, N = 200, 333
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 2))
+    cuts = [0, 1, 100, 101, 333]
+    parts = [tsg.tcsc_slice(*t.arrays, N, a, b) for a, b in zip(cuts, cuts[1:])]
+    Wd = np.concatenate([O.TCSC(*p, K, b - a).dense() for p, (a, b) in zip(parts, zip(cuts, cuts[1:]))], 1)
+    assert np.array_equal(Wd, t.dense())
+
+
+@pytest.mark.parametrize("bad", ["oob", "unsorted", "both", "start", "monotone"])
+def test_validate_rejects(tsg, bad):
+    csp, csn = np.array([0, 2, 3]), np.array([0, 1, 1])
+    rip, rin = np.array([0, 3, 1]), np.array([2])
+    tsg.validate(csp, csn, rip, rin, 4, 2)
+    if bad == "oob":
+        rip = np.array([0, 4, 1])
+    elif bad == "unsorted":
+        rip = np.array([3, 0, 1])
+    elif bad == "both":
+        rin = np.array([3])
+    elif bad == "start":
+        csn = np.array([1, 1, 1])
+    elif bad == "monotone":
+        csp = np.array([0, 3, 2])
+    with pytest.raises(tsg.TSGError) as e:
+        tsg.validate(csp, csn, rip, rin, 4, 2)
+    assert e.value.code == 1
+
+
+def test_registry_mirrors_main_cpp(tsg):
+    tsg.clear_registry()
+    f = lambda X, B, Y, M, N, K: None  # noqa: E731
+    tsg.add_function(f, "HipBaseTCSC")
+    tsg.add_prelu_function(f, "HipBaseTCSC_PreLU")
+    assert tsg.funcNames == ["HipBaseTCSC"] and tsg.userFuncs == [f]
+    assert tsg.funcNames_prelu == ["HipBaseTCSC_PreLU"]
+    tsg.clear_registry()
+
+
+def test_metrics_formulas(tsg):
+    # readme.md:84-85 / SURVEY 8(d): cfg1 flops 33,685,504; cfg3 bytes 402,849,800
+    assert tsg.flops(32, 4096, 1024 * 4096 // 4) == 33_685_504
+    assert tsg.algorithmic_bytes(4096, 16384, 4096, 4096 * 16384 // 4) == 402_849_800
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-GPU error path")
+def test_no_gpu_fails_loudly(tsg, oracle_mod):
+    t = oracle_mod.tcsc_encode(np.eye(4, dtype=np.int32))
+    with pytest.raises(tsg.TSGError) as e:
+        tsg.TCSCDevice(*t.arrays, 4, 4)
+    assert e.value.code == 4  # TSG_ERR_NODEV: never a silent CPU fallback
