@@ -150,7 +150,7 @@ def main():
 
     if rank == 0:
         flops_all = M * (nnz_all + Ntot)  # sum over ranks of T.flops(M, Nr, nnz_rank)
-        value = flops_all / elapsed_max / 1e9
+        value = flops_all * a.steps / elapsed_max / 1e9
         ms_step = elapsed_max / a.steps * 1e3
         alg_bytes = T.algorithmic_bytes(M, Nr, K, nnz)  # per launch, this rank
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9

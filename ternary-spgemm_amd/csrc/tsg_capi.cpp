@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -30,7 +31,9 @@ static int fail(int code, const std::string &msg)
 struct tsg_tcsc {
     int K = 0, N = 0, device = 0;
     int64_t nnz_pos = 0, nnz_neg = 0;
-    tsg::Image img;                       // host copy of the device image
+    bool stream_kernel = true;            // TSG_KERNEL=chunked selects the round-1 v1 kernel
+    tsg::Image img;                       // v1 device image (chunked kernel)
+    tsg::StreamImage simg;                // device image of the stream kernel
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
@@ -78,7 +81,7 @@ int check_device(int dev)
 int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp)
 {
     Mp = ((std::max(M, 1) + tsg::kTileM - 1) / tsg::kTileM) * tsg::kTileM;
-    Kp = h->img.nch * tsg::kChunkK;
+    Kp = h->stream_kernel ? h->simg.nch * tsg::kSChunk : h->img.nch * tsg::kChunkK;
     return TSG_OK;
 }
 
@@ -155,8 +158,12 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         slot = h->ring_head;
         HIP_TRY(hipEventRecord(h->ev0[slot], s));
     }
-    if (tsg::launch_tcsc(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->img.Npad,
-                         h->img.nch, h->img.tile_cols, prelu ? 1 : 0, s) != 0)
+    const int lrc = h->stream_kernel
+        ? tsg::launch_tcsc_stream(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N,
+                                  h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, s)
+        : tsg::launch_tcsc(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->img.Npad,
+                           h->img.nch, h->img.tile_cols, prelu ? 1 : 0, s);
+    if (lrc != 0)
         return fail(TSG_ERR_HIP, std::string("tcsc launch: ") + hipGetErrorString(hipGetLastError()));
     if (slot >= 0) {
         HIP_TRY(hipEventRecord(h->ev1[slot], s));
@@ -261,18 +268,29 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     h->csn.assign(csn, csn + N + 1);
     if (h->nnz_pos) h->rip.assign(rip, rip + h->nnz_pos);
     if (h->nnz_neg) h->rin.assign(rin, rin + h->nnz_neg);
-    tsg::build_image(csp, csn, rip, rin, K, N, tsg::pick_tile_cols(N), h->img);
+    const char *kenv = std::getenv("TSG_KERNEL");
+    h->stream_kernel = !(kenv && std::strcmp(kenv, "chunked") == 0);
+    const std::vector<uint32_t> *segv, *entv;
+    if (h->stream_kernel) {
+        tsg::build_stream_image(csp, csn, rip, rin, K, N, tsg::pick_stream_nw(N), h->simg);
+        segv = &h->simg.wstart;
+        entv = &h->simg.ent;
+    } else {
+        tsg::build_image(csp, csn, rip, rin, K, N, tsg::pick_tile_cols(N), h->img);
+        segv = &h->img.seg;
+        entv = &h->img.ent;
+    }
 
     DeviceGuard g(device);
-    const size_t sb = h->img.seg.size() * sizeof(uint32_t), eb = h->img.ent.size() * sizeof(uint32_t);
+    const size_t sb = segv->size() * sizeof(uint32_t), eb = entv->size() * sizeof(uint32_t);
     if (hipMalloc(&h->d_seg, sb) != hipSuccess || hipMalloc(&h->d_ent, eb) != hipSuccess ||
         hipMalloc(&h->d_b, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
         hipMalloc(&h->d_alpha, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess) {
         free_handle(h);
         return fail(TSG_ERR_NOMEM, "hipMalloc of the device image failed");
     }
-    if (hipMemcpy(h->d_seg, h->img.seg.data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->d_ent, h->img.ent.data(), eb, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(h->d_seg, segv->data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->d_ent, entv->data(), eb, hipMemcpyHostToDevice) != hipSuccess) {
         free_handle(h);
         return fail(TSG_ERR_HIP, "upload of the device image failed");
     }
@@ -347,11 +365,12 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     o->nnz_pos = h->nnz_pos;
     o->nnz_neg = h->nnz_neg;
     o->tcsc_bytes = 4 * (2 * ((int64_t)h->N + 1) + h->nnz_pos + h->nnz_neg);
-    o->image_bytes = (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;
+    o->image_bytes = h->stream_kernel ? (int64_t)(h->simg.wstart.size() + h->simg.ent.size()) * 4
+                                      : (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;
-    o->chunk_rows = tsg::kChunkK;
+    o->chunk_rows = h->stream_kernel ? tsg::kSChunk : tsg::kChunkK;
     o->tile_rows = tsg::kTileM;
-    o->tile_cols = h->img.tile_cols;
+    o->tile_cols = h->stream_kernel ? h->simg.tile_cols : h->img.tile_cols;
     return TSG_OK;
 }
 

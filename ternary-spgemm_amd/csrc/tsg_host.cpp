@@ -64,6 +64,79 @@ void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
     img.ent.resize(img.ent.size() + 64, 0u);  // tail: keeps any over-fetch in bounds
 }
 
+int pick_stream_nw(int N)
+{
+    // kSWaves waves x nw columns per workgroup tile
+    return N <= kSWaves * 8 ? 8 : 16;
+}
+
+void build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                        const int32_t *rin, int K, int N, int nw, StreamImage &img)
+{
+    img.K = K;
+    img.N = N;
+    img.nw = nw;
+    img.tile_cols = kSWaves * nw;
+    img.Npad = ((N + img.tile_cols - 1) / img.tile_cols) * img.tile_cols;
+    img.nch = std::max(1, (K + kSChunk - 1) / kSChunk);
+    const int nch = img.nch, ntiles = img.Npad / img.tile_cols;
+    const int hdr_words = nw / kEntPerWord;
+    img.wstart.assign((size_t)ntiles * kSWaves, 0u);
+    img.ent.clear();
+    const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
+    img.ent.reserve((size_t)(nnz / kEntPerWord) * 5 / 4 + (size_t)img.Npad * 2 * nch + 256);
+
+    std::vector<int32_t> cur((size_t)nw * 2);  // per column & pass: next row index
+    for (int t = 0; t < ntiles; t++) {
+        for (int w = 0; w < kSWaves; w++) {
+            const int n0 = t * img.tile_cols + w * nw;
+            if (img.ent.size() & 1) img.ent.push_back(0u);
+            img.wstart[(size_t)t * kSWaves + w] = (uint32_t)img.ent.size();
+            for (int c = 0; c < nw; c++)
+                for (int p = 0; p < 2; p++) {
+                    const int n = n0 + c;
+                    cur[(size_t)c * 2 + p] = n < N ? (p ? csn[n] : csp[n]) : 0;
+                }
+            for (int q = 0; q < 2 * nch; q++) {
+                const int p = q / nch, j = q % nch;
+                const uint32_t par = (uint32_t)(q & 1) << 7;
+                const int32_t *cs = p ? csn : csp;
+                const int32_t *ri = p ? rin : rip;
+                if (img.ent.size() & 1) img.ent.push_back(0u);
+                const size_t hdr = img.ent.size();
+                img.ent.resize(hdr + hdr_words, 0u);
+                for (int c = 0; c < nw; c++) {
+                    if (img.ent.size() & 1) img.ent.push_back(0u);  // segments start 8-byte aligned
+                    const int n = n0 + c;
+                    int32_t &i = cur[(size_t)c * 2 + p];
+                    const int32_t e = n < N ? cs[n + 1] : 0;
+                    const int32_t khi = (j + 1) * kSChunk;
+                    const size_t seg0 = img.ent.size();
+                    uint32_t word = 0;
+                    int fill = 0;
+                    while (i < e && ri[i] < khi) {
+                        word |= ((uint32_t)(ri[i] - j * kSChunk) | par) << (8 * fill);
+                        if (++fill == kEntPerWord) {
+                            img.ent.push_back(word);
+                            word = 0;
+                            fill = 0;
+                        }
+                        i++;
+                    }
+                    if (fill) {
+                        for (; fill < kEntPerWord; fill++)
+                            word |= ((uint32_t)kSZeroRow | par) << (8 * fill);
+                        img.ent.push_back(word);
+                    }
+                    const uint32_t cnt = (uint32_t)(img.ent.size() - seg0);  // <= 32
+                    img.ent[hdr + c / kEntPerWord] |= cnt << (8 * (c % kEntPerWord));
+                }
+            }
+        }
+    }
+    img.ent.resize(img.ent.size() + 64, 0u);  // the one-step scalar prefetch may run past the end
+}
+
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                           const int32_t *rin, int K, int N)
 {

@@ -9,47 +9,67 @@
 
 namespace tsg {
 
-// Geometry of the LDS kernel (csrc/tcsc_kernels.hip).  The device image is
-// built for exactly this geometry at registration.
-constexpr int kLanes = 64;          // wavefront width (CDNA)
-constexpr int kRowsPerLane = 2;     // M rows one lane accumulates (float2 = ds_read_b64)
+constexpr int kLanes = 64;                     // wavefront width (CDNA)
+constexpr int kRowsPerLane = 2;                // M rows one lane accumulates (float2 = ds_read_b64)
 constexpr int kTileM = kLanes * kRowsPerLane;  // 128 M rows per workgroup
+constexpr int kEntPerWord = 4;                 // uint8 entries per dword
+
+// ---------------------------------------------------------------------------
+// "stream" kernel (tsg_tcsc_stream_kernel, the default)
+//
+// LDS image of one X^T chunk, double buffered, 128 KiB:
+//   byte(buf, half, row, l) = half*65536 + buf*32768 + row*256 + l*8
+// with lane = 32*half + l owning M rows m0 + 2*lane + {0,1}.  An entry byte
+// e = row | buf<<7 is byte 1 of that address, the lane constant supplies
+// bytes 0 and 2, so ONE v_perm_b32 turns a packed entry into the ds_read_b64
+// address (no scalar ALU per entry).  Row kZeroRow of each buffer holds +0.0f.
+constexpr int kSChunk = 127;        // K rows per chunk (row 127 = zero row)
+constexpr int kSZeroRow = 127;
+constexpr int kSWaves = 16;         // waves per workgroup (1024 threads, 1 WG per CU)
+constexpr int kSLdsBytes = 131072;
+
+// Entry stream of one wave: for every chunk step q = p*nch + j (p = 0: the
+// +1 runs over all K chunks, then p = 1: the -1 runs), a header of NW bytes
+// (dword count of each of the wave's NW column segments, NW/4 dwords), then
+// the NW segments: entries (k - j*kSChunk) | (q&1)<<7, ascending k, 4 per
+// dword, the last dword padded with kSZeroRow | (q&1)<<7.
+struct StreamImage {
+    int K = 0, N = 0, Npad = 0, nch = 0;
+    int nw = 0;                     // columns per wave
+    int tile_cols = 0;              // kSWaves * nw
+    std::vector<uint32_t> wstart;   // per (column tile, wave): first dword of its stream
+    std::vector<uint32_t> ent;      // all streams (+ tail padding)
+};
+void build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                        const int32_t *rin, int K, int N, int nw, StreamImage &img);
+int pick_stream_nw(int N);
+
+// ---------------------------------------------------------------------------
+// "chunked" kernel (tsg_tcsc_lds_kernel, round-1 v1, kept for A/B)
 constexpr int kChunkK = 128;        // K rows of X^T staged in LDS per chunk
 constexpr int kZeroRow = kChunkK;   // LDS row holding +0.0f (pads index groups)
 constexpr int kWaves = 4;           // waves per workgroup (256 threads)
-constexpr int kEntPerWord = 4;      // uint8 row-in-chunk entries per dword
 
-// Device image of one TCSC ("chunked TCSC"): for column n, pass p (0 = the
-// +1 run, 1 = the -1 run) and K-chunk j, the entries of that column whose k
-// lies in [j*kChunkK, (j+1)*kChunkK), in ascending k (the TCSC order), as
-// uint8 (k - j*kChunkK), packed 4 per dword, the group padded with kZeroRow.
-//   seg[((n*2 + p) * (nch+1)) + j]  = first dword of (n, p, j);
-//   seg[... + j + 1]               = one past its last dword.
-// Columns are padded to a multiple of the workgroup column tile with empty
-// segments.  Entries for (n,p) are contiguous over j, so seg has nch+1 values.
 struct Image {
     int K = 0, N = 0, Npad = 0, nch = 0;
     int tile_cols = 0;
     std::vector<uint32_t> seg;   // Npad * 2 * (nch + 1)
-    std::vector<uint32_t> ent;   // packed entries (+ kEntTail dwords of padding)
+    std::vector<uint32_t> ent;   // packed entries (+ tail padding)
 };
-
-// Builds the image from TCSC arrays (assumed validated).  tile_cols = N
-// columns per workgroup; Npad = roundup(N, tile_cols).
 void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                  const int32_t *rin, int K, int N, int tile_cols, Image &img);
+int pick_tile_cols(int N);
 
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                           const int32_t *rin, int K, int N);
 
 // Kernel launchers (csrc/tcsc_kernels.hip).  All enqueue on `stream`.
-// Mp/Kp: padded dims of the X^T work buffer (Mp % kTileM == 0, Kp = nch*kChunkK).
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream);
 int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *ent,
                 const float *b, const float *alpha, float *Y, int M, int N, int Npad,
                 int nch, int tile_cols, int prelu, void *stream);
-
-// Workgroup column tile used for an image (a function of N only).
-int pick_tile_cols(int N);
+int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
+                       const float *b, const float *alpha, float *Y, int M, int N, int Npad,
+                       int nch, int nw, int prelu, void *stream);
 
 }  // namespace tsg
