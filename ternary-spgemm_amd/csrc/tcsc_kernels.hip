@@ -30,7 +30,7 @@ namespace tsg {
 // ------------------------------------------------------------------ kernel 1 --
 __global__ __launch_bounds__(256) void tsg_transpose_kernel(const float *__restrict__ X,
                                                             float *__restrict__ XT, int M, int K,
-                                                            int Mp)
+                                                            int Mp, int Kp)
 {
     __shared__ float tile[64][65];
     const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void tsg_transpose_kernel(const float *__restr
 #pragma unroll
     for (int i = 0; i < 16; i++) {
         const int k = k0 + ty + 4 * i, m = m0 + tx;
-        XT[(size_t)k * Mp + m] = tile[tx][ty + 4 * i];
+        if (k < Kp) XT[(size_t)k * Mp + m] = tile[tx][ty + 4 * i];
     }
 }
 
@@ -153,15 +153,40 @@ __global__ __launch_bounds__(256, 2) void tsg_tcsc_lds_kernel(
 }
 
 // ------------------------------------------------------------------ kernel 3 --
-// tsg_tcsc_stream_kernel: one 1024-thread workgroup per CU (128 KiB LDS),
-// 16 waves x NW columns, 128 M rows.  Double-buffered X^T chunks of 127 K rows.
-// Each wave walks ONE linear entry stream (see StreamImage) with scalar loads
-// (two dwords = 8 entries per s_load, prefetched one step ahead so the SMEM
-// latency hides under the previous step's LDS reads), and one v_perm_b32 per
-// entry turns the packed byte into the ds_read_b64 address: per entry the
-// vector ALU does 2 instructions (perm + pk_add/sub), the scalar ALU none.
+// tsg_tcsc_stream_kernel (default).  One 1024-thread workgroup per CU, the
+// whole 160 KiB LDS:
+//   [0, 128 KiB)      X^T chunk (127 K rows x 128 M rows), double buffered,
+//                     byte(buf, half, row, l) = half*65536 + buf*32768 + row*256 + l*8;
+//   [128, 160 KiB)    per wave, double buffered, 1 KiB of its entry stream.
+// Step q (= p*nch + j: the +1 runs over all K chunks, then the -1 runs) is
+// staged during step q-1 by LDS-DMA (global_load_lds_dwordx4, no VGPRs): the
+// X^T chunk (4 pieces of 1 KiB per wave) and each wave's sub-stream (1 piece).
+// A wave then walks its NW column segments; an entry byte e = row | buf<<7 is
+// byte 1 of its LDS address, so one v_perm_b32 with the lane constant
+// (bytes 0 and 2) forms each ds_read_b64 address.  Per entry: v_perm,
+// ds_read_b64, v_pk_add/sub; per 8 entries one broadcast ds_read_b64 of
+// index bytes.  Bound: LDS read bandwidth.
 
-// address of entry I (0..3) of packed dword w: byte1 <- entry, bytes 0/2 <- lane constant
+// One LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS
+// [lds_dst, lds_dst + 1 KiB).  Inline asm on purpose: hipcc cannot prove that
+// later ds_reads do not alias an in-flight LDS-DMA and would put
+// `s_waitcnt vmcnt(0)` in front of the first one (serialising the prefetch).
+// The kernel waits for these itself (vmcnt(0) before each step's barrier);
+// M0 is set and restored inside the statement (cdna_hip_programming.md 5.7).
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst)
+{
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
 template <int I>
 __device__ __forceinline__ uint32_t entry_addr(uint32_t w, uint32_t lanec)
 {
@@ -174,14 +199,29 @@ __device__ __forceinline__ float2 lds_f2(const char *lds, uint32_t a)
 }
 
 template <bool NEG>
-__device__ __forceinline__ float2 walk_column(float2 a, const uint32_t *__restrict__ p, uint32_t cnt,
-                                              uint32_t lanec, const char *lds)
+__device__ __forceinline__ float2 walk_quad(float2 a, uint32_t w, uint32_t lanec, const char *lds)
+{
+    const float2 x0 = lds_f2(lds, entry_addr<0>(w, lanec));
+    const float2 x1 = lds_f2(lds, entry_addr<1>(w, lanec));
+    const float2 x2 = lds_f2(lds, entry_addr<2>(w, lanec));
+    const float2 x3 = lds_f2(lds, entry_addr<3>(w, lanec));
+    a = chain_step<NEG>(a, x0);
+    a = chain_step<NEG>(a, x1);
+    a = chain_step<NEG>(a, x2);
+    a = chain_step<NEG>(a, x3);
+    return a;
+}
+
+// Segment of `cnt` dwords at LDS byte `ipos` (8-byte aligned).
+template <bool NEG>
+__device__ __forceinline__ float2 walk_column(float2 a, uint32_t ipos, uint32_t cnt, uint32_t lanec,
+                                              const char *lds)
 {
     if (cnt == 0) return a;
-    uint2 w = *reinterpret_cast<const uint2 *>(p);  // segment starts are 8-byte aligned
+    uint2 w = *reinterpret_cast<const uint2 *>(lds + ipos);  // broadcast read
     uint32_t i = 0;
     for (; i + 2 <= cnt; i += 2) {
-        const uint2 nx = *reinterpret_cast<const uint2 *>(p + i + 2);  // prefetch (tail padded)
+        const uint2 nx = *reinterpret_cast<const uint2 *>(lds + ipos + 4 * (i + 2));  // prefetch
         const float2 x0 = lds_f2(lds, entry_addr<0>(w.x, lanec));
         const float2 x1 = lds_f2(lds, entry_addr<1>(w.x, lanec));
         const float2 x2 = lds_f2(lds, entry_addr<2>(w.x, lanec));
@@ -200,81 +240,63 @@ __device__ __forceinline__ float2 walk_column(float2 a, const uint32_t *__restri
         a = chain_step<NEG>(a, x7);
         w = nx;
     }
-    if (i < cnt) {
-        const float2 x0 = lds_f2(lds, entry_addr<0>(w.x, lanec));
-        const float2 x1 = lds_f2(lds, entry_addr<1>(w.x, lanec));
-        const float2 x2 = lds_f2(lds, entry_addr<2>(w.x, lanec));
-        const float2 x3 = lds_f2(lds, entry_addr<3>(w.x, lanec));
-        a = chain_step<NEG>(a, x0);
-        a = chain_step<NEG>(a, x1);
-        a = chain_step<NEG>(a, x2);
-        a = chain_step<NEG>(a, x3);
-    }
+    if (i < cnt) a = walk_quad<NEG>(a, w.x, lanec, lds);
     return a;
 }
 
-// One chunk step of one wave: header (NW dword counts, NW/4 dwords), then the
-// NW segments, each starting on an even dword.  Returns the next step's start.
-template <int NW, bool NEG>
-__device__ __forceinline__ const uint32_t *walk_chunk(float2 (&acc)[NW], const uint32_t *__restrict__ p,
-                                                      uint32_t lanec, const char *lds)
-{
-    uint32_t hdr[NW / 4];
-#pragma unroll
-    for (int i = 0; i < NW / 4; i++) hdr[i] = p[i];
-    p += NW / 4;
-#pragma unroll
-    for (int c = 0; c < NW; c++) {
-        const uint32_t cnt = (hdr[c / 4] >> (8 * (c % 4))) & 0xffu;
-        acc[c] = walk_column<NEG>(acc[c], p, cnt, lanec, lds);
-        p += (cnt + 1) & ~1u;
-    }
-    return p;
-}
-
-// X^T chunk (127 rows x 128 M) -> registers (4 float4 per thread)
-struct ChunkRegs {
-    float4 v[4];
+template <int NW>
+struct StreamHeader {
+    static constexpr int kWords = ((1 + NW / 4) + 1) & ~1;  // len + counts, even
 };
 
-__device__ __forceinline__ void load_chunk(ChunkRegs &r, const float *__restrict__ XT, int Mp,
-                                           int m0, int j, int tid)
+template <int NW, bool NEG>
+__device__ __forceinline__ void walk_chunk(float2 (&acc)[NW], const uint32_t (&cw)[NW / 4],
+                                           uint32_t ibase, uint32_t lanec, const char *lds)
 {
+    uint32_t ipos = ibase + 4u * StreamHeader<NW>::kWords;
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int i = tid + 1024 * t;  // < 127*32 = 4064 valid
-        const int row = i >> 5, c4 = i & 31;
-        if (row < kSChunk)
-            r.v[t] = *reinterpret_cast<const float4 *>(XT + (size_t)(j * kSChunk + row) * Mp + m0 + 4 * c4);
+    for (int c = 0; c < NW; c++) {
+        const uint32_t cnt = (cw[c / 4] >> (8 * (c % 4))) & 0xffu;
+        acc[c] = walk_column<NEG>(acc[c], ipos, cnt, lanec, lds);
+        ipos += 4u * ((cnt + 1) & ~1u);
     }
 }
 
-__device__ __forceinline__ void store_chunk(const ChunkRegs &r, char *lds, int buf, int tid)
+// LDS-DMA of X^T chunk j (127 rows x 128 M) into buffer `buf`: 64 pieces of
+// 1 KiB (4 rows of one half), 4 per wave; row 127 (the zero row) is sourced
+// from a zeroed global buffer so every refill also re-zeroes it.
+__device__ __forceinline__ void stage_x(const float *__restrict__ XT, const float *__restrict__ zero,
+                                        int Mp, int m0, int j, int buf, int wave, int lane)
 {
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int i = tid + 1024 * t;
-        const int row = i >> 5, c4 = i & 31;
-        if (row < kSChunk) {
-            const uint32_t a = (uint32_t)((c4 >> 4) * 65536 + buf * 32768 + row * 256 + (c4 & 15) * 16);
-            *reinterpret_cast<float4 *>(lds + a) = r.v[t];
-        }
+    for (int i = 0; i < 4; i++) {
+        const int p = wave * 4 + i;
+        const int h = p >> 5, r0 = (p & 31) * 4, rr = r0 + (lane >> 4), mo = (lane & 15) * 4;
+        const float *src = rr < kSChunk ? XT + (size_t)(j * kSChunk + rr) * Mp + m0 + 64 * h + mo
+                                        : zero + mo;
+        glds16(src, (uint32_t)(h * 65536 + buf * 32768 + r0 * 256));
     }
+}
+
+__device__ __forceinline__ void stage_idx(const uint32_t *__restrict__ ent, uint32_t base,
+                                          uint32_t dst, int lane)
+{
+    glds16(ent + base + 4 * lane, dst);
 }
 
 template <int NW, bool PRELU>
 __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wstart,
-    const uint32_t *__restrict__ ent, const float *__restrict__ b,
+    const uint32_t *__restrict__ ent, const float *__restrict__ zero, const float *__restrict__ b,
     const float *__restrict__ alpha, float *__restrict__ Y, int M, int N, int nch, int mtiles,
     int ntiles)
 {
-    __shared__ __attribute__((aligned(16))) char lds[kSLdsBytes];
+    __shared__ __attribute__((aligned(16))) char lds[kSLdsBytes + kSIdxBytes];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     // XCD-aware bijective remap: blocks b and b+8 share an XCD (observed
-    // round-robin dispatch); give each XCD a contiguous run of m-tile-major
+    // round-robin dispatch); each XCD gets a contiguous, m-tile-major run of
     // tiles so its concurrent workgroups share the X^T slab in L2.  Speed only.
     const int T = mtiles * ntiles, L = blockIdx.x;
     const int xcd = L & 7, slot = L >> 3, q8 = T >> 3, r8 = T & 7;
@@ -284,32 +306,42 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
     const int ncol0 = nt * (kSWaves * NW) + wave * NW;
 
     const uint32_t lanec = ((uint32_t)(lane & 31) << 3) | ((uint32_t)(lane >> 5) << 16);
+    const uint32_t ireg = (uint32_t)kSLdsBytes + (uint32_t)wave * 2u * kSIdxWaveBytes;  // + buf*1KiB
 
-    // zero rows: row 127 of both buffers and both halves (4 x 256 B)
-    if (tid < 256) {
-        const int h = tid >> 7, bf = (tid >> 6) & 1, x = tid & 63;
-        reinterpret_cast<float *>(lds + h * 65536 + bf * 32768 + kSZeroRow * 256)[x] = 0.0f;
-    }
-    ChunkRegs cr;
-    load_chunk(cr, XT, Mp, m0, 0, tid);
-    store_chunk(cr, lds, 0, tid);
-
-    const uint32_t *sp = ent + wstart[(size_t)nt * kSWaves + wave];
+    uint32_t sbase = wstart[(size_t)nt * kSWaves + wave];
+    stage_x(XT, zero, Mp, m0, 0, 0, wave, lane);
+    stage_idx(ent, sbase, ireg, lane);
 
     float2 acc[NW];
 #pragma unroll
     for (int c = 0; c < NW; c++) acc[c] = make_float2(0.0f, 0.0f);  // comp.h:41
+
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
     const int steps = 2 * nch;
     for (int q = 0; q < steps; q++) {
-        const bool more = q + 1 < steps;
-        if (more) load_chunk(cr, XT, Mp, m0, (q + 1) % nch, tid);
-        // the entry bytes carry the buffer bit, so both buffers share one base
-        if (q < nch) sp = walk_chunk<NW, false>(acc, sp, lanec, lds);  // +1 runs, ascending K
-        else sp = walk_chunk<NW, true>(acc, sp, lanec, lds);           // -1 runs, ascending K
-        if (more) store_chunk(cr, lds, (q + 1) & 1, tid);
-        __syncthreads();
+        const uint32_t ib = ireg + (uint32_t)(q & 1) * kSIdxWaveBytes;
+        // header of this step: [len][NW count bytes]
+        uint32_t hw[StreamHeader<NW>::kWords];
+#pragma unroll
+        for (int i = 0; i < StreamHeader<NW>::kWords; i += 2) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(lds + ib + 4 * i);
+            hw[i] = __builtin_amdgcn_readfirstlane(v.x);
+            hw[i + 1] = __builtin_amdgcn_readfirstlane(v.y);
+        }
+        if (q + 1 < steps) {  // stage step q+1 into the other buffers
+            sbase += hw[0];
+            stage_x(XT, zero, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
+            stage_idx(ent, sbase, ireg + (uint32_t)((q + 1) & 1) * kSIdxWaveBytes, lane);
+        }
+        uint32_t cw[NW / 4];
+#pragma unroll
+        for (int i = 0; i < NW / 4; i++) cw[i] = hw[1 + i];
+        if (q < nch) walk_chunk<NW, false>(acc, cw, ib, lanec, lds);  // +1 runs, ascending K
+        else walk_chunk<NW, true>(acc, cw, ib, lanec, lds);           // -1 runs, ascending K
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA for q+1 landed
+        __syncthreads();                                   // ... and every other wave's
     }
 
     if (ncol0 >= N) return;
@@ -341,8 +373,8 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
 // ---------------------------------------------------------------- launchers --
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream)
 {
-    dim3 grid((unsigned)(Kp / 64), (unsigned)(Mp / 64));
-    hipLaunchKernelGGL(tsg_transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, XT, M, K, Mp);
+    dim3 grid((unsigned)((Kp + 63) / 64), (unsigned)(Mp / 64));
+    hipLaunchKernelGGL(tsg_transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream, X, XT, M, K, Mp, Kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -376,29 +408,31 @@ int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *en
 
 template <int NW, bool PRELU>
 static void launch_stream_nw(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
-                             const float *b, const float *alpha, float *Y, int M, int N, int Npad,
-                             int nch, hipStream_t s)
+                             const float *zero, const float *b, const float *alpha, float *Y, int M,
+                             int N, int Npad, int nch, hipStream_t s)
 {
     const int mtiles = Mp / kTileM, ntiles = Npad / (kSWaves * NW);
     hipLaunchKernelGGL((tsg_tcsc_stream_kernel<NW, PRELU>), dim3((unsigned)(mtiles * ntiles)),
-                       dim3(1024), 0, s, XT, Mp, wstart, ent, b, alpha, Y, M, N, nch, mtiles, ntiles);
+                       dim3(1024), 0, s, XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, nch, mtiles,
+                       ntiles);
 }
 
 int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
-                       const float *b, const float *alpha, float *Y, int M, int N, int Npad,
-                       int nch, int nw, int prelu, void *stream)
+                       const float *zero, const float *b, const float *alpha, float *Y, int M,
+                       int N, int Npad, int nch, int nw, int prelu, void *stream)
 {
     hipStream_t s = (hipStream_t)stream;
-    if (nw == 16) {
-        if (prelu) launch_stream_nw<16, true>(XT, Mp, wstart, ent, b, alpha, Y, M, N, Npad, nch, s);
-        else launch_stream_nw<16, false>(XT, Mp, wstart, ent, b, alpha, Y, M, N, Npad, nch, s);
-    } else if (nw == 8) {
-        if (prelu) launch_stream_nw<8, true>(XT, Mp, wstart, ent, b, alpha, Y, M, N, Npad, nch, s);
-        else launch_stream_nw<8, false>(XT, Mp, wstart, ent, b, alpha, Y, M, N, Npad, nch, s);
-    } else {
-        return -2;
+#define TSG_NW(NWV)                                                                               \
+    if (nw == NWV) {                                                                              \
+        if (prelu) launch_stream_nw<NWV, true>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, s); \
+        else launch_stream_nw<NWV, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, s); \
+        return hipGetLastError() == hipSuccess ? 0 : -1;                                          \
     }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    TSG_NW(16)
+    TSG_NW(8)
+    TSG_NW(4)
+#undef TSG_NW
+    return -2;
 }
 
 }  // namespace tsg

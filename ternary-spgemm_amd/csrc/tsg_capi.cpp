@@ -37,6 +37,7 @@ struct tsg_tcsc {
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
+    float *d_zero = nullptr;              // 256 B of +0.0f (source of the LDS zero rows)
     size_t work_bytes = 0;
     // host-pointer path staging (tcsc_hip_gemm): grow-only
     float *d_x = nullptr, *d_b = nullptr, *d_y = nullptr, *d_alpha = nullptr;
@@ -159,7 +160,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         HIP_TRY(hipEventRecord(h->ev0[slot], s));
     }
     const int lrc = h->stream_kernel
-        ? tsg::launch_tcsc_stream(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N,
+        ? tsg::launch_tcsc_stream(h->d_work, Mp, h->d_seg, h->d_ent, h->d_zero, db, dalpha, dY, M, N,
                                   h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, s)
         : tsg::launch_tcsc(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->img.Npad,
                            h->img.nch, h->img.tile_cols, prelu ? 1 : 0, s);
@@ -214,7 +215,7 @@ void free_handle(tsg_tcsc *h)
     if (!h) return;
     DeviceGuard g(h->device);
     if (h->ring_count) (void)hipDeviceSynchronize();
-    for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_x,
+    for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_zero, (void *)h->d_x,
                     (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha})
         if (p) (void)hipFree(p);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -272,7 +273,7 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     h->stream_kernel = !(kenv && std::strcmp(kenv, "chunked") == 0);
     const std::vector<uint32_t> *segv, *entv;
     if (h->stream_kernel) {
-        tsg::build_stream_image(csp, csn, rip, rin, K, N, tsg::pick_stream_nw(N), h->simg);
+        tsg::plan_stream_image(csp, csn, rip, rin, K, N, h->simg);
         segv = &h->simg.wstart;
         entv = &h->simg.ent;
     } else {
@@ -285,11 +286,13 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     const size_t sb = segv->size() * sizeof(uint32_t), eb = entv->size() * sizeof(uint32_t);
     if (hipMalloc(&h->d_seg, sb) != hipSuccess || hipMalloc(&h->d_ent, eb) != hipSuccess ||
         hipMalloc(&h->d_b, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
-        hipMalloc(&h->d_alpha, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess) {
+        hipMalloc(&h->d_alpha, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
+        hipMalloc(&h->d_zero, 256) != hipSuccess) {
         free_handle(h);
         return fail(TSG_ERR_NOMEM, "hipMalloc of the device image failed");
     }
-    if (hipMemcpy(h->d_seg, segv->data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemset(h->d_zero, 0, 256) != hipSuccess ||
+        hipMemcpy(h->d_seg, segv->data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->d_ent, entv->data(), eb, hipMemcpyHostToDevice) != hipSuccess) {
         free_handle(h);
         return fail(TSG_ERR_HIP, "upload of the device image failed");

@@ -64,14 +64,8 @@ void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
     img.ent.resize(img.ent.size() + 64, 0u);  // tail: keeps any over-fetch in bounds
 }
 
-int pick_stream_nw(int N)
-{
-    // kSWaves waves x nw columns per workgroup tile
-    return N <= kSWaves * 8 ? 8 : 16;
-}
-
-void build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                        const int32_t *rin, int K, int N, int nw, StreamImage &img)
+int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                       const int32_t *rin, int K, int N, int nw, StreamImage &img)
 {
     img.K = K;
     img.N = N;
@@ -80,17 +74,19 @@ void build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *r
     img.Npad = ((N + img.tile_cols - 1) / img.tile_cols) * img.tile_cols;
     img.nch = std::max(1, (K + kSChunk - 1) / kSChunk);
     const int nch = img.nch, ntiles = img.Npad / img.tile_cols;
-    const int hdr_words = nw / kEntPerWord;
+    const int hdr_words = ((1 + nw / kEntPerWord) + 1) & ~1;
     img.wstart.assign((size_t)ntiles * kSWaves, 0u);
     img.ent.clear();
     const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
-    img.ent.reserve((size_t)(nnz / kEntPerWord) * 5 / 4 + (size_t)img.Npad * 2 * nch + 256);
+    img.ent.reserve((size_t)(nnz / kEntPerWord) * 5 / 4 + (size_t)img.Npad * 2 * nch * 2 + 512);
+    int maxsub = 0;
 
+    auto align = [&](size_t a) { while (img.ent.size() % a) img.ent.push_back(0u); };
     std::vector<int32_t> cur((size_t)nw * 2);  // per column & pass: next row index
     for (int t = 0; t < ntiles; t++) {
         for (int w = 0; w < kSWaves; w++) {
             const int n0 = t * img.tile_cols + w * nw;
-            if (img.ent.size() & 1) img.ent.push_back(0u);
+            align(4);
             img.wstart[(size_t)t * kSWaves + w] = (uint32_t)img.ent.size();
             for (int c = 0; c < nw; c++)
                 for (int p = 0; p < 2; p++) {
@@ -102,11 +98,11 @@ void build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *r
                 const uint32_t par = (uint32_t)(q & 1) << 7;
                 const int32_t *cs = p ? csn : csp;
                 const int32_t *ri = p ? rin : rip;
-                if (img.ent.size() & 1) img.ent.push_back(0u);
-                const size_t hdr = img.ent.size();
-                img.ent.resize(hdr + hdr_words, 0u);
+                align(4);  // sub-stream: 16-byte aligned for the LDS-DMA piece
+                const size_t sub0 = img.ent.size();
+                img.ent.resize(sub0 + hdr_words, 0u);
                 for (int c = 0; c < nw; c++) {
-                    if (img.ent.size() & 1) img.ent.push_back(0u);  // segments start 8-byte aligned
+                    align(2);  // segment: 8-byte aligned for ds_read_b64
                     const int n = n0 + c;
                     int32_t &i = cur[(size_t)c * 2 + p];
                     const int32_t e = n < N ? cs[n + 1] : 0;
@@ -123,18 +119,34 @@ void build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *r
                         }
                         i++;
                     }
-                    if (fill) {
+                    if (fill) {  // pad the last group with the +0.0f row of this buffer
                         for (; fill < kEntPerWord; fill++)
                             word |= ((uint32_t)kSZeroRow | par) << (8 * fill);
                         img.ent.push_back(word);
                     }
                     const uint32_t cnt = (uint32_t)(img.ent.size() - seg0);  // <= 32
-                    img.ent[hdr + c / kEntPerWord] |= cnt << (8 * (c % kEntPerWord));
+                    img.ent[sub0 + 1 + c / kEntPerWord] |= cnt << (8 * (c % kEntPerWord));
                 }
+                align(2);
+                const size_t len = img.ent.size() - sub0;
+                img.ent[sub0] = (uint32_t)len;
+                maxsub = std::max(maxsub, (int)len);
             }
         }
     }
-    img.ent.resize(img.ent.size() + 64, 0u);  // the one-step scalar prefetch may run past the end
+    align(4);
+    img.ent.resize(img.ent.size() + kSSubMax + 64, 0u);  // a 1 KiB DMA piece may run past the end
+    return maxsub;
+}
+
+void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                       const int32_t *rin, int K, int N, StreamImage &img)
+{
+    for (int nw : {16, 8}) {
+        if (nw == 16 && N <= kSWaves * 8) continue;  // tiny N: narrower tiles waste less
+        if (build_stream_image(csp, csn, rip, rin, K, N, nw, img) <= kSSubMax) return;
+    }
+    build_stream_image(csp, csn, rip, rin, K, N, 4, img);  // 2 + 4*32 dwords always fit
 }
 
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,

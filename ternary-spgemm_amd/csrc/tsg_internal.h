@@ -26,13 +26,19 @@ constexpr int kEntPerWord = 4;                 // uint8 entries per dword
 constexpr int kSChunk = 127;        // K rows per chunk (row 127 = zero row)
 constexpr int kSZeroRow = 127;
 constexpr int kSWaves = 16;         // waves per workgroup (1024 threads, 1 WG per CU)
-constexpr int kSLdsBytes = 131072;
+constexpr int kSLdsBytes = 131072;     // X^T double buffer
+constexpr int kSIdxWaveBytes = 1024;   // per wave per buffer: 256 dwords of entry stream
+constexpr int kSIdxBytes = kSWaves * 2 * kSIdxWaveBytes;  // 32 KiB -> 160 KiB in all
+constexpr int kSSubMax = kSIdxWaveBytes / 4;             // max dwords of one step's sub-stream
 
 // Entry stream of one wave: for every chunk step q = p*nch + j (p = 0: the
-// +1 runs over all K chunks, then p = 1: the -1 runs), a header of NW bytes
-// (dword count of each of the wave's NW column segments, NW/4 dwords), then
-// the NW segments: entries (k - j*kSChunk) | (q&1)<<7, ascending k, 4 per
-// dword, the last dword padded with kSZeroRow | (q&1)<<7.
+// +1 runs over all K chunks, then p = 1: the -1 runs) a sub-stream starting
+// on a 16-byte boundary: header [total dwords of the sub-stream][NW count
+// bytes = dwords of each column segment] padded to an even length, then the
+// NW segments (each starting on an even dword): entries
+// (k - j*kSChunk) | (q&1)<<7, ascending k, 4 per dword, the last dword padded
+// with kSZeroRow | (q&1)<<7.  A sub-stream is at most kSSubMax dwords; the
+// planner lowers nw (16 -> 8 -> 4) until that holds.
 struct StreamImage {
     int K = 0, N = 0, Npad = 0, nch = 0;
     int nw = 0;                     // columns per wave
@@ -40,9 +46,13 @@ struct StreamImage {
     std::vector<uint32_t> wstart;   // per (column tile, wave): first dword of its stream
     std::vector<uint32_t> ent;      // all streams (+ tail padding)
 };
-void build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                        const int32_t *rin, int K, int N, int nw, StreamImage &img);
-int pick_stream_nw(int N);
+// Returns the largest sub-stream (dwords); callers retry with a smaller nw
+// when it exceeds kSSubMax.
+int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                       const int32_t *rin, int K, int N, int nw, StreamImage &img);
+// Builds with the widest nw (16, 8, 4) whose sub-streams fit.
+void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                       const int32_t *rin, int K, int N, StreamImage &img);
 
 // ---------------------------------------------------------------------------
 // "chunked" kernel (tsg_tcsc_lds_kernel, round-1 v1, kept for A/B)
@@ -69,7 +79,7 @@ int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *en
                 const float *b, const float *alpha, float *Y, int M, int N, int Npad,
                 int nch, int tile_cols, int prelu, void *stream);
 int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
-                       const float *b, const float *alpha, float *Y, int M, int N, int Npad,
-                       int nch, int nw, int prelu, void *stream);
+                       const float *zero, const float *b, const float *alpha, float *Y, int M,
+                       int N, int Npad, int nch, int nw, int prelu, void *stream);
 
 }  // namespace tsg
