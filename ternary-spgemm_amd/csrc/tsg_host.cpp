@@ -127,7 +127,7 @@ int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
                     const uint32_t cnt = (uint32_t)(img.ent.size() - seg0);  // <= 32
                     img.ent[sub0 + 1 + c / kEntPerWord] |= cnt << (8 * (c % kEntPerWord));
                 }
-                align(2);
+                align(4);  // len is the exact distance to the next sub-stream
                 const size_t len = img.ent.size() - sub0;
                 img.ent[sub0] = (uint32_t)len;
                 maxsub = std::max(maxsub, (int)len);
