@@ -244,6 +244,62 @@ __device__ __forceinline__ float2 walk_column(float2 a, uint32_t ipos, uint32_t 
     return a;
 }
 
+// Two columns walked in lockstep for min(ca, cb) dwords: two independent
+// chains per wave interleave their LDS latency; each chain keeps its own
+// order.  The longer column finishes alone.
+template <bool NEG>
+__device__ __forceinline__ void walk_pair(float2 &acc_a, float2 &acc_b, uint32_t pa, uint32_t ca,
+                                          uint32_t pb, uint32_t cb, uint32_t lanec, const char *lds)
+{
+    const uint32_t joint = ca < cb ? ca : cb;
+    float2 a = acc_a, b = acc_b;
+    uint32_t i = 0;
+    if (joint >= 2) {
+        uint2 wa = *reinterpret_cast<const uint2 *>(lds + pa);
+        uint2 wb = *reinterpret_cast<const uint2 *>(lds + pb);
+        for (; i + 2 <= joint; i += 2) {
+            const uint2 na = *reinterpret_cast<const uint2 *>(lds + pa + 4 * (i + 2));
+            const uint2 nb = *reinterpret_cast<const uint2 *>(lds + pb + 4 * (i + 2));
+            const float2 x0 = lds_f2(lds, entry_addr<0>(wa.x, lanec));
+            const float2 y0 = lds_f2(lds, entry_addr<0>(wb.x, lanec));
+            const float2 x1 = lds_f2(lds, entry_addr<1>(wa.x, lanec));
+            const float2 y1 = lds_f2(lds, entry_addr<1>(wb.x, lanec));
+            const float2 x2 = lds_f2(lds, entry_addr<2>(wa.x, lanec));
+            const float2 y2 = lds_f2(lds, entry_addr<2>(wb.x, lanec));
+            const float2 x3 = lds_f2(lds, entry_addr<3>(wa.x, lanec));
+            const float2 y3 = lds_f2(lds, entry_addr<3>(wb.x, lanec));
+            const float2 x4 = lds_f2(lds, entry_addr<0>(wa.y, lanec));
+            const float2 y4 = lds_f2(lds, entry_addr<0>(wb.y, lanec));
+            const float2 x5 = lds_f2(lds, entry_addr<1>(wa.y, lanec));
+            const float2 y5 = lds_f2(lds, entry_addr<1>(wb.y, lanec));
+            const float2 x6 = lds_f2(lds, entry_addr<2>(wa.y, lanec));
+            const float2 y6 = lds_f2(lds, entry_addr<2>(wb.y, lanec));
+            const float2 x7 = lds_f2(lds, entry_addr<3>(wa.y, lanec));
+            const float2 y7 = lds_f2(lds, entry_addr<3>(wb.y, lanec));
+            a = chain_step<NEG>(a, x0);
+            b = chain_step<NEG>(b, y0);
+            a = chain_step<NEG>(a, x1);
+            b = chain_step<NEG>(b, y1);
+            a = chain_step<NEG>(a, x2);
+            b = chain_step<NEG>(b, y2);
+            a = chain_step<NEG>(a, x3);
+            b = chain_step<NEG>(b, y3);
+            a = chain_step<NEG>(a, x4);
+            b = chain_step<NEG>(b, y4);
+            a = chain_step<NEG>(a, x5);
+            b = chain_step<NEG>(b, y5);
+            a = chain_step<NEG>(a, x6);
+            b = chain_step<NEG>(b, y6);
+            a = chain_step<NEG>(a, x7);
+            b = chain_step<NEG>(b, y7);
+            wa = na;
+            wb = nb;
+        }
+    }
+    acc_a = walk_column<NEG>(a, pa + 4 * i, ca - i, lanec, lds);
+    acc_b = walk_column<NEG>(b, pb + 4 * i, cb - i, lanec, lds);
+}
+
 template <int NW>
 struct StreamHeader {
     static constexpr int kWords = ((1 + NW / 4) + 1) & ~1;  // len + counts, even
@@ -253,13 +309,17 @@ template <int NW, bool NEG>
 __device__ __forceinline__ void walk_chunk(float2 (&acc)[NW], const uint32_t (&cw)[NW / 4],
                                            uint32_t ibase, uint32_t lanec, const char *lds)
 {
+    uint32_t pos[NW], cnt[NW];
     uint32_t ipos = ibase + 4u * StreamHeader<NW>::kWords;
 #pragma unroll
     for (int c = 0; c < NW; c++) {
-        const uint32_t cnt = (cw[c / 4] >> (8 * (c % 4))) & 0xffu;
-        acc[c] = walk_column<NEG>(acc[c], ipos, cnt, lanec, lds);
-        ipos += 4u * ((cnt + 1) & ~1u);
+        cnt[c] = (cw[c / 4] >> (8 * (c % 4))) & 0xffu;
+        pos[c] = ipos;
+        ipos += 4u * ((cnt[c] + 1) & ~1u);
     }
+#pragma unroll
+    for (int c = 0; c < NW; c += 2)
+        walk_pair<NEG>(acc[c], acc[c + 1], pos[c], cnt[c], pos[c + 1], cnt[c + 1], lanec, lds);
 }
 
 // LDS-DMA of X^T chunk j (127 rows x 128 M) into buffer `buf`: 64 pieces of
