@@ -344,13 +344,17 @@ __device__ __forceinline__ void stage_idx(const uint32_t *__restrict__ ent, uint
     glds16(ent + base + 4 * lane, dst);
 }
 
-template <int NW, bool PRELU>
+// STAMP: diagnostic build only (TSG_STAMPS=1): per wave, s_memtime cycles
+// spent walking vs. waiting at the step barrier, written to `stamps`.
+template <int NW, bool PRELU, bool STAMP>
 __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wstart,
     const uint32_t *__restrict__ ent, const float *__restrict__ zero, const float *__restrict__ b,
     const float *__restrict__ alpha, float *__restrict__ Y, int M, int N, int nch, int mtiles,
-    int ntiles)
+    int ntiles, unsigned long long *__restrict__ stamps)
 {
+    unsigned long long st_work = 0, st_wait = 0, st_t0 = 0;
+    if (STAMP) st_t0 = __builtin_amdgcn_s_memtime();
     __shared__ __attribute__((aligned(16))) char lds[kSLdsBytes + kSIdxBytes];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -381,6 +385,8 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
 
     const int steps = 2 * nch;
     for (int q = 0; q < steps; q++) {
+        unsigned long long ta = 0, tb = 0;
+        if (STAMP) ta = __builtin_amdgcn_s_memtime();
         const uint32_t ib = ireg + (uint32_t)(q & 1) * kSIdxWaveBytes;
         // header of this step: [len][NW count bytes]
         uint32_t hw[StreamHeader<NW>::kWords];
@@ -400,8 +406,24 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
         for (int i = 0; i < NW / 4; i++) cw[i] = hw[1 + i];
         if (q < nch) walk_chunk<NW, false>(acc, cw, ib, lanec, lds);  // +1 runs, ascending K
         else walk_chunk<NW, true>(acc, cw, ib, lanec, lds);           // -1 runs, ascending K
+        if (STAMP) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            tb = __builtin_amdgcn_s_memtime();
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA for q+1 landed
         __syncthreads();                                   // ... and every other wave's
+        if (STAMP) {
+            const unsigned long long tc = __builtin_amdgcn_s_memtime();
+            st_work += tb - ta;
+            st_wait += tc - tb;
+        }
+    }
+    if (STAMP && lane == 0) {
+        unsigned long long *o = stamps + ((size_t)blockIdx.x * kSWaves + wave) * 4;
+        o[0] = st_work;
+        o[1] = st_wait;
+        o[2] = __builtin_amdgcn_s_memtime() - st_t0;
+        o[3] = (unsigned long long)((nt << 16) | mt);
     }
 
     if (ncol0 >= N) return;
@@ -466,26 +488,28 @@ int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *en
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int NW, bool PRELU>
+template <int NW, bool PRELU, bool STAMP>
 static void launch_stream_nw(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                              const float *zero, const float *b, const float *alpha, float *Y, int M,
-                             int N, int Npad, int nch, hipStream_t s)
+                             int N, int Npad, int nch, unsigned long long *stamps, hipStream_t s)
 {
     const int mtiles = Mp / kTileM, ntiles = Npad / (kSWaves * NW);
-    hipLaunchKernelGGL((tsg_tcsc_stream_kernel<NW, PRELU>), dim3((unsigned)(mtiles * ntiles)),
+    hipLaunchKernelGGL((tsg_tcsc_stream_kernel<NW, PRELU, STAMP>), dim3((unsigned)(mtiles * ntiles)),
                        dim3(1024), 0, s, XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, nch, mtiles,
-                       ntiles);
+                       ntiles, stamps);
 }
 
 int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                        const float *zero, const float *b, const float *alpha, float *Y, int M,
-                       int N, int Npad, int nch, int nw, int prelu, void *stream)
+                       int N, int Npad, int nch, int nw, int prelu, unsigned long long *stamps,
+                       void *stream)
 {
     hipStream_t s = (hipStream_t)stream;
 #define TSG_NW(NWV)                                                                               \
     if (nw == NWV) {                                                                              \
-        if (prelu) launch_stream_nw<NWV, true>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, s); \
-        else launch_stream_nw<NWV, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, s); \
+        if (stamps) launch_stream_nw<NWV, false, true>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, stamps, s); \
+        else if (prelu) launch_stream_nw<NWV, true, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, nullptr, s); \
+        else launch_stream_nw<NWV, false, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, nullptr, s); \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                          \
     }
     TSG_NW(16)

@@ -159,13 +159,37 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         slot = h->ring_head;
         HIP_TRY(hipEventRecord(h->ev0[slot], s));
     }
+    unsigned long long *stamps = nullptr;
+    size_t nstamp = 0;
+    if (h->stream_kernel && std::getenv("TSG_STAMPS")) {  // diagnostic build path (never timed)
+        nstamp = (size_t)(Mp / tsg::kTileM) * (h->simg.Npad / h->simg.tile_cols) * tsg::kSWaves * 4;
+        HIP_TRY(hipMalloc(&stamps, nstamp * 8));
+    }
     const int lrc = h->stream_kernel
         ? tsg::launch_tcsc_stream(h->d_work, Mp, h->d_seg, h->d_ent, h->d_zero, db, dalpha, dY, M, N,
-                                  h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, s)
+                                  h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, stamps, s)
         : tsg::launch_tcsc(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->img.Npad,
                            h->img.nch, h->img.tile_cols, prelu ? 1 : 0, s);
     if (lrc != 0)
         return fail(TSG_ERR_HIP, std::string("tcsc launch: ") + hipGetErrorString(hipGetLastError()));
+    if (stamps) {
+        std::vector<unsigned long long> hs(nstamp);
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipMemcpy(hs.data(), stamps, nstamp * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(stamps));
+        double work = 0, wait = 0, tot = 0, wmax = 0;
+        const size_t nw = nstamp / 4;
+        for (size_t i = 0; i < nw; i++) {
+            work += (double)hs[4 * i];
+            wait += (double)hs[4 * i + 1];
+            tot += (double)hs[4 * i + 2];
+            wmax = std::max(wmax, (double)hs[4 * i]);
+        }
+        std::fprintf(stderr, "[tsg stamps] waves=%zu mean cycles/wave: total %.0f walk %.0f (%.1f%%) "
+                             "barrier-wait %.0f (%.1f%%) max-walk %.0f steps=%d\n",
+                     nw, tot / nw, work / nw, 100 * work / tot, wait / nw, 100 * wait / tot, wmax,
+                     2 * h->simg.nch);
+    }
     if (slot >= 0) {
         HIP_TRY(hipEventRecord(h->ev1[slot], s));
         h->ring_head = (h->ring_head + 1) % tsg_tcsc::kRing;

@@ -80,6 +80,7 @@ int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *en
                 int nch, int tile_cols, int prelu, void *stream);
 int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                        const float *zero, const float *b, const float *alpha, float *Y, int M,
-                       int N, int Npad, int nch, int nw, int prelu, void *stream);
+                       int N, int Npad, int nch, int nw, int prelu, unsigned long long *stamps,
+                       void *stream);
 
 }  // namespace tsg

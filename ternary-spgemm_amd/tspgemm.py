@@ -25,7 +25,7 @@ from typing import Callable, List, Optional, Tuple
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libternary_spgemm.so")
+LIB_PATH = os.environ.get("TSG_LIB") or os.path.join(PKG_DIR, "lib", "libternary_spgemm.so")
 
 TSG_OK = 0
 _ERRNAMES = {1: "TSG_ERR_ARG", 2: "TSG_ERR_HIP", 3: "TSG_ERR_NOMEM", 4: "TSG_ERR_NODEV",
