@@ -27,6 +27,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ternary-spgemm_amd"))
 
 import tspgemm as T  # noqa: E402
+import tsg_dist as D  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 PROFILE_PMC = os.path.join(REPO, "profiles", "r01_pmc_summary.json")
@@ -66,7 +67,8 @@ def main():
 
     M, K, Nr, s = a.M, a.K, a.N, a.s
     Ntot = Nr * world
-    n0, n1 = rank * Nr, (rank + 1) * Nr
+    n0, n1 = D.column_shard(Ntot, world, rank)  # == [rank*Nr, (rank+1)*Nr)
+    assert n1 - n0 == Nr
 
     # --- synthetic inputs (generateSparseMatrix law), this rank's column shard
     t0 = time.time()
@@ -117,13 +119,12 @@ def main():
     # optional: all-gather of Y column blocks over RCCL (outside the timed region)
     allgather_ms = None
     if a.allgather and world > 1:
-        Yall = torch.empty((world, M, Nr), device=dev)
-        dist.all_gather_into_tensor(Yall, Y)
+        Yall = D.allgather_columns(Y, Ntot, world)  # warm RCCL
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
         for _ in range(3):
-            dist.all_gather_into_tensor(Yall, Y)
+            Yall = D.allgather_columns(Y, Ntot, world)
         torch.cuda.synchronize()
         allgather_ms = (time.perf_counter() - t1) / 3 * 1e3
         del Yall

@@ -318,8 +318,17 @@ __device__ __forceinline__ void walk_chunk(float2 (&acc)[NW], const uint32_t (&c
         ipos += 4u * ((cnt[c] + 1) & ~1u);
     }
 #pragma unroll
-    for (int c = 0; c < NW; c += 2)
+    for (int c = 0; c < NW; c += 2) {
+#ifdef TSG_PRIO
+        // progress-based priority: a wave that is further through its chunk
+        // yields the issue ports to waves that lag, so the 16 waves reach
+        // the step barrier together instead of leaving a latency-bound tail
+        if (c == NW / 4) __builtin_amdgcn_s_setprio(2);
+        if (c == NW / 2) __builtin_amdgcn_s_setprio(1);
+        if (c == 3 * NW / 4) __builtin_amdgcn_s_setprio(0);
+#endif
         walk_pair<NEG>(acc[c], acc[c + 1], pos[c], cnt[c], pos[c + 1], cnt[c + 1], lanec, lds);
+    }
 }
 
 // LDS-DMA of X^T chunk j (127 rows x 128 M) into buffer `buf`: 64 pieces of
@@ -388,6 +397,9 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
         unsigned long long ta = 0, tb = 0;
         if (STAMP) ta = __builtin_amdgcn_s_memtime();
         const uint32_t ib = ireg + (uint32_t)(q & 1) * kSIdxWaveBytes;
+#ifdef TSG_PRIO
+        __builtin_amdgcn_s_setprio(3);
+#endif
         // header of this step: [len][NW count bytes]
         uint32_t hw[StreamHeader<NW>::kWords];
 #pragma unroll
