@@ -212,35 +212,63 @@ __device__ __forceinline__ float2 walk_quad(float2 a, uint32_t w, uint32_t lanec
     return a;
 }
 
-// Segment of `cnt` dwords at LDS byte `ipos` (8-byte aligned).
+// Tail of a segment: 1..3 entries of the dword at `ipos` (no padded reads).
 template <bool NEG>
-__device__ __forceinline__ float2 walk_column(float2 a, uint32_t ipos, uint32_t cnt, uint32_t lanec,
-                                              const char *lds)
+__device__ __forceinline__ float2 walk_tail(float2 a, uint32_t ipos, uint32_t t, uint32_t lanec,
+                                            const char *lds)
 {
-    if (cnt == 0) return a;
-    uint2 w = *reinterpret_cast<const uint2 *>(lds + ipos);  // broadcast read
-    uint32_t i = 0;
-    for (; i + 2 <= cnt; i += 2) {
-        const uint2 nx = *reinterpret_cast<const uint2 *>(lds + ipos + 4 * (i + 2));  // prefetch
-        const float2 x0 = lds_f2(lds, entry_addr<0>(w.x, lanec));
-        const float2 x1 = lds_f2(lds, entry_addr<1>(w.x, lanec));
-        const float2 x2 = lds_f2(lds, entry_addr<2>(w.x, lanec));
-        const float2 x3 = lds_f2(lds, entry_addr<3>(w.x, lanec));
-        const float2 x4 = lds_f2(lds, entry_addr<0>(w.y, lanec));
-        const float2 x5 = lds_f2(lds, entry_addr<1>(w.y, lanec));
-        const float2 x6 = lds_f2(lds, entry_addr<2>(w.y, lanec));
-        const float2 x7 = lds_f2(lds, entry_addr<3>(w.y, lanec));
-        a = chain_step<NEG>(a, x0);
+    const uint32_t w = *reinterpret_cast<const uint32_t *>(lds + ipos);  // broadcast read
+    const float2 x0 = lds_f2(lds, entry_addr<0>(w, lanec));
+    a = chain_step<NEG>(a, x0);
+    if (t > 1) {
+        const float2 x1 = lds_f2(lds, entry_addr<1>(w, lanec));
         a = chain_step<NEG>(a, x1);
-        a = chain_step<NEG>(a, x2);
-        a = chain_step<NEG>(a, x3);
-        a = chain_step<NEG>(a, x4);
-        a = chain_step<NEG>(a, x5);
-        a = chain_step<NEG>(a, x6);
-        a = chain_step<NEG>(a, x7);
-        w = nx;
+        if (t > 2) {
+            const float2 x2 = lds_f2(lds, entry_addr<2>(w, lanec));
+            a = chain_step<NEG>(a, x2);
+        }
     }
-    if (i < cnt) a = walk_quad<NEG>(a, w.x, lanec, lds);
+    return a;
+}
+
+// Segment of `ne` entries (ne/4 full dwords + a tail) at LDS byte `ipos`
+// (8-byte aligned), starting at full dword `i0`.
+template <bool NEG>
+__device__ __forceinline__ float2 walk_column(float2 a, uint32_t ipos, uint32_t ne, uint32_t i0,
+                                              uint32_t lanec, const char *lds)
+{
+    const uint32_t full = ne >> 2;
+    uint32_t i = i0;
+    if (i + 2 <= full) {
+        uint2 w = *reinterpret_cast<const uint2 *>(lds + ipos + 4 * i);  // broadcast read
+        for (; i + 2 <= full; i += 2) {
+            const uint2 nx = *reinterpret_cast<const uint2 *>(lds + ipos + 4 * (i + 2));  // prefetch
+            const float2 x0 = lds_f2(lds, entry_addr<0>(w.x, lanec));
+            const float2 x1 = lds_f2(lds, entry_addr<1>(w.x, lanec));
+            const float2 x2 = lds_f2(lds, entry_addr<2>(w.x, lanec));
+            const float2 x3 = lds_f2(lds, entry_addr<3>(w.x, lanec));
+            const float2 x4 = lds_f2(lds, entry_addr<0>(w.y, lanec));
+            const float2 x5 = lds_f2(lds, entry_addr<1>(w.y, lanec));
+            const float2 x6 = lds_f2(lds, entry_addr<2>(w.y, lanec));
+            const float2 x7 = lds_f2(lds, entry_addr<3>(w.y, lanec));
+            a = chain_step<NEG>(a, x0);
+            a = chain_step<NEG>(a, x1);
+            a = chain_step<NEG>(a, x2);
+            a = chain_step<NEG>(a, x3);
+            a = chain_step<NEG>(a, x4);
+            a = chain_step<NEG>(a, x5);
+            a = chain_step<NEG>(a, x6);
+            a = chain_step<NEG>(a, x7);
+            w = nx;
+        }
+    }
+    if (i < full) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(lds + ipos + 4 * i);
+        a = walk_quad<NEG>(a, w, lanec, lds);
+        i++;
+    }
+    const uint32_t t = ne & 3u;
+    if (t) a = walk_tail<NEG>(a, ipos + 4 * i, t, lanec, lds);
     return a;
 }
 
@@ -248,9 +276,10 @@ __device__ __forceinline__ float2 walk_column(float2 a, uint32_t ipos, uint32_t 
 // chains per wave interleave their LDS latency; each chain keeps its own
 // order.  The longer column finishes alone.
 template <bool NEG>
-__device__ __forceinline__ void walk_pair(float2 &acc_a, float2 &acc_b, uint32_t pa, uint32_t ca,
-                                          uint32_t pb, uint32_t cb, uint32_t lanec, const char *lds)
+__device__ __forceinline__ void walk_pair(float2 &acc_a, float2 &acc_b, uint32_t pa, uint32_t ea,
+                                          uint32_t pb, uint32_t eb, uint32_t lanec, const char *lds)
 {
+    const uint32_t ca = ea >> 2, cb = eb >> 2;  // full dwords
     const uint32_t joint = ca < cb ? ca : cb;
     float2 a = acc_a, b = acc_b;
     uint32_t i = 0;
@@ -296,8 +325,8 @@ __device__ __forceinline__ void walk_pair(float2 &acc_a, float2 &acc_b, uint32_t
             wb = nb;
         }
     }
-    acc_a = walk_column<NEG>(a, pa + 4 * i, ca - i, lanec, lds);
-    acc_b = walk_column<NEG>(b, pb + 4 * i, cb - i, lanec, lds);
+    acc_a = walk_column<NEG>(a, pa, ea, i, lanec, lds);
+    acc_b = walk_column<NEG>(b, pb, eb, i, lanec, lds);
 }
 
 template <int NW>
@@ -313,9 +342,9 @@ __device__ __forceinline__ void walk_chunk(float2 (&acc)[NW], const uint32_t (&c
     uint32_t ipos = ibase + 4u * StreamHeader<NW>::kWords;
 #pragma unroll
     for (int c = 0; c < NW; c++) {
-        cnt[c] = (cw[c / 4] >> (8 * (c % 4))) & 0xffu;
+        cnt[c] = (cw[c / 4] >> (8 * (c % 4))) & 0xffu;  // entries (exact)
         pos[c] = ipos;
-        ipos += 4u * ((cnt[c] + 1) & ~1u);
+        ipos += 4u * ((((cnt[c] + 3) >> 2) + 1) & ~1u);   // dwords, even-aligned
     }
 #pragma unroll
     for (int c = 0; c < NW; c += 2) {

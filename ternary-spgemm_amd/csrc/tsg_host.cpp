@@ -107,10 +107,10 @@ int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
                     int32_t &i = cur[(size_t)c * 2 + p];
                     const int32_t e = n < N ? cs[n + 1] : 0;
                     const int32_t khi = (j + 1) * kSChunk;
-                    const size_t seg0 = img.ent.size();
-                    uint32_t word = 0;
+                    uint32_t word = 0, nent = 0;
                     int fill = 0;
                     while (i < e && ri[i] < khi) {
+                        nent++;
                         word |= ((uint32_t)(ri[i] - j * kSChunk) | par) << (8 * fill);
                         if (++fill == kEntPerWord) {
                             img.ent.push_back(word);
@@ -124,8 +124,8 @@ int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
                             word |= ((uint32_t)kSZeroRow | par) << (8 * fill);
                         img.ent.push_back(word);
                     }
-                    const uint32_t cnt = (uint32_t)(img.ent.size() - seg0);  // <= 32
-                    img.ent[sub0 + 1 + c / kEntPerWord] |= cnt << (8 * (c % kEntPerWord));
+                    // exact entry count (<= kSChunk): the kernel reads no padding
+                    img.ent[sub0 + 1 + c / kEntPerWord] |= nent << (8 * (c % kEntPerWord));
                 }
                 align(4);  // len is the exact distance to the next sub-stream
                 const size_t len = img.ent.size() - sub0;

@@ -34,7 +34,7 @@ constexpr int kSSubMax = kSIdxWaveBytes / 4;             // max dwords of one st
 // Entry stream of one wave: for every chunk step q = p*nch + j (p = 0: the
 // +1 runs over all K chunks, then p = 1: the -1 runs) a sub-stream starting
 // on a 16-byte boundary: header [total dwords of the sub-stream][NW count
-// bytes = dwords of each column segment] padded to an even length, then the
+// bytes = entries of each column segment] padded to an even length, then the
 // NW segments (each starting on an even dword): entries
 // (k - j*kSChunk) | (q&1)<<7, ascending k, 4 per dword, the last dword padded
 // with kSZeroRow | (q&1)<<7.  A sub-stream is at most kSSubMax dwords; the
