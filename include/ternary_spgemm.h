@@ -52,6 +52,14 @@ int tcsc_hip_create(const int32_t *col_start_pos, const int32_t *col_start_neg,
  * TCSC.h:13-41; any value other than +1/-1 is treated as 0, as there). */
 int tcsc_hip_create_dense(const int32_t *W, int K, int N, int device, tsg_tcsc **out);
 
+/* Same, from "CSC with compressed values vector (1s and -1s, 8 bits for 5
+ * values)" (readme.md:111, the reference's optimisation idea 2): col_ptr
+ * int32[N+1], row_idx int32[nnz] (ascending k per column), values base-3
+ * packed 5 per byte in CSC order, digit = v + 1.  Results are the same
+ * BaseTCSC chains (+1 entries, then -1 entries, each ascending). */
+int tcsc_hip_create_csc_packed(const int32_t *col_ptr, const int32_t *row_idx,
+                               const uint8_t *packed, int K, int N, int device, tsg_tcsc **out);
+
 /* Releases every device/host resource of the handle (NULL is a no-op). */
 void tcsc_hip_destroy(tsg_tcsc *h);
 
@@ -130,6 +138,17 @@ int tsg_tcsc_validate(const int32_t *col_start_pos, const int32_t *col_start_neg
 int tsg_gen_tcsc(int K, int N, int s, uint64_t seed, int n0, int n1,
                  int32_t *csp, int32_t *csn, int32_t *rip, int32_t *rin,
                  int64_t *nnz_pos, int64_t *nnz_neg);
+
+/* Format conversions between TCSC and CSC + base-3 packed values (see
+ * tcsc_hip_create_csc_packed).  NULL outputs query the sizes only.
+ * packed has ceil(nnz/5) bytes. */
+int tsg_tcsc_to_csc_packed(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                           const int32_t *row_index_pos, const int32_t *row_index_neg, int N,
+                           int32_t *col_ptr, int32_t *row_idx, uint8_t *packed, int64_t *nnz);
+int tsg_csc_packed_to_tcsc(const int32_t *col_ptr, const int32_t *row_idx, const uint8_t *packed,
+                           int N, int32_t *col_start_pos, int32_t *col_start_neg,
+                           int32_t *row_index_pos, int32_t *row_index_neg, int64_t *nnz_pos,
+                           int64_t *nnz_neg);
 
 /* X[i] = integer-valued fp32 U{-range..range} (initX, sparseUtils.h:6-23). */
 int tsg_gen_x(int64_t len, int range, uint64_t seed, float *X);

@@ -53,6 +53,12 @@ def lib() -> C.CDLL:
         L.oracle_base_tcsc_prelu.argtypes = kargs[:6] + [_f32p] + kargs[6:]
         L.oracle_base_blocked_tcsc.argtypes = kargs + [C.c_int]
         L.oracle_gemm_dense.argtypes = [_f32p, _f32p, _f32p, _f32p, C.c_int, C.c_int, C.c_int]
+        _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+        L.oracle_csc_packed_encode.argtypes = [_i32p, C.c_int, C.c_int, _i32p, _i32p, _u8p]
+        L.oracle_csc_packed_encode.restype = None
+        L.oracle_base_csc_packed.argtypes = [_f32p, _i32p, _i32p, _u8p, _f32p, _f32p,
+                                             C.c_int, C.c_int, C.c_int]
+        L.oracle_base_csc_packed.restype = None
         for f in ("oracle_gen_ternary", "oracle_init_x_int", "oracle_init_x_frac",
                   "oracle_tcsc_count", "oracle_tcsc_encode", "oracle_tcsc_decode",
                   "oracle_blocked_tcsc_encode", "oracle_base_tcsc", "oracle_base_tcsc_omp",
@@ -170,6 +176,29 @@ def blocked_tcsc_encode(W: np.ndarray, B: int):
     rin = np.empty(max(q.value, 1), np.int32)
     lib().oracle_blocked_tcsc_encode(W, K, N, B, csp, csn, rip, rin)
     return csp, csn, rip[: p.value].copy(), rin[: q.value].copy()
+
+
+def csc_packed_encode(W: np.ndarray):
+    """CSC + base-3 packed values, 5 per byte (readme.md:111)."""
+    W = np.ascontiguousarray(W, dtype=np.int32)
+    K, N = W.shape
+    nnz = int(np.count_nonzero((W == 1) | (W == -1)))
+    col_ptr = np.empty(N + 1, np.int32)
+    row_idx = np.empty(max(nnz, 1), np.int32)
+    packed = np.zeros(max((nnz + 4) // 5, 1), np.uint8)
+    lib().oracle_csc_packed_encode(W, K, N, col_ptr, row_idx, packed)
+    return col_ptr, row_idx[:nnz].copy(), packed[: (nnz + 4) // 5].copy()
+
+
+def base_csc_packed(X, col_ptr, row_idx, packed, b, K: int, N: int) -> np.ndarray:
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    b = np.ascontiguousarray(b, dtype=np.float32)
+    M = X.shape[0]
+    Y = np.empty((M, N), np.float32)
+    ri = row_idx if len(row_idx) else np.zeros(1, np.int32)
+    pk = packed if len(packed) else np.zeros(1, np.uint8)
+    lib().oracle_base_csc_packed(X, np.ascontiguousarray(col_ptr, np.int32), ri, pk, b, Y, M, N, K)
+    return Y
 
 
 # ---------------------------------------------------------------- kernels --

@@ -157,6 +157,33 @@ void oracle_blocked_tcsc_encode(const int32_t *W, int K, int N, int B,
     csn[slot] = cn;
 }
 
+void oracle_csc_packed_encode(const int32_t *W, int K, int N, int32_t *col_ptr, int32_t *row_idx,
+                              uint8_t *packed)
+{
+    static const int pw[5] = {1, 3, 9, 27, 81};
+    int64_t e = 0;
+    for (int n = 0; n < N; n++) {
+        col_ptr[n] = (int32_t)e;
+        for (int k = 0; k < K; k++) {
+            const int32_t v = W[(size_t)k * N + n];
+            if (v == 1 || v == -1) {
+                row_idx[e] = k;
+                if (e % 5 == 0) packed[e / 5] = 0;
+                packed[e / 5] = (uint8_t)(packed[e / 5] + (v + 1) * pw[e % 5]);
+                e++;
+            }
+        }
+    }
+    col_ptr[N] = (int32_t)e;
+}
+
+int oracle_csc_packed_value(const uint8_t *packed, int64_t i)
+{
+    int b = packed[i / 5];
+    for (int j = 0; j < (int)(i % 5); j++) b /= 3;
+    return b % 3 - 1;
+}
+
 /* ----------------------------------------------------------------- kernels -- */
 
 static inline float base_tcsc_one(const float *xrow, const int32_t *csp, const int32_t *csn,
@@ -309,6 +336,22 @@ void oracle_base_blocked_tcsc(const float *X, const int32_t *csp, const int32_t 
             }
         }
         for (int n = 0; n < N; n++) yrow[n] += b[n]; /* :648-654 */
+    }
+}
+
+void oracle_base_csc_packed(const float *X, const int32_t *col_ptr, const int32_t *row_idx,
+                            const uint8_t *packed, const float *b, float *Y, int M, int N, int K)
+{
+    for (int m = 0; m < M; m++) {
+        const float *xrow = X + (size_t)m * K;
+        for (int n = 0; n < N; n++) {
+            float y = 0.0f;
+            for (int32_t i = col_ptr[n]; i < col_ptr[n + 1]; i++)
+                if (oracle_csc_packed_value(packed, i) == 1) y += xrow[row_idx[i]];
+            for (int32_t i = col_ptr[n]; i < col_ptr[n + 1]; i++)
+                if (oracle_csc_packed_value(packed, i) == -1) y -= xrow[row_idx[i]];
+            Y[(size_t)m * N + n] = y + b[n];
+        }
     }
 }
 

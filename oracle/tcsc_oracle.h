@@ -81,6 +81,15 @@ void oracle_blocked_tcsc_encode(const int32_t *W, int K, int N, int B,
                                 int32_t *col_start_pos, int32_t *col_start_neg,
                                 int32_t *row_index_pos, int32_t *row_index_neg);
 
+/* "CSC with compressed values vector (1s and -1s, 8 bits for 5 values)"
+ * (readme.md:111, optimisation idea 2; no reference implementation exists):
+ * col_ptr int32[N+1], row_idx int32[nnz] ascending k per column (+1 and -1
+ * merged), values base-3 packed 5 per byte in CSC order, digit = v + 1
+ * (so -1 -> 0, +1 -> 2), byte = d0 + 3 d1 + 9 d2 + 27 d3 + 81 d4. */
+void oracle_csc_packed_encode(const int32_t *W, int K, int N, int32_t *col_ptr, int32_t *row_idx,
+                              uint8_t *packed);
+int oracle_csc_packed_value(const uint8_t *packed, int64_t i); /* -1 / 0 / +1 */
+
 /* ---- kernels ---------------------------------------------------------------- */
 
 /* BaseTCSC<float> (comp.h:25-69), same order: y=0; y+=X[m,k] over the +1 run
@@ -115,6 +124,11 @@ void oracle_base_tcsc_prelu(const float *X, const int32_t *col_start_pos, const 
 void oracle_base_blocked_tcsc(const float *X, const int32_t *col_start_pos, const int32_t *col_start_neg,
                               const int32_t *row_index_pos, const int32_t *row_index_neg,
                               const float *b, float *Y, int M, int N, int K, int B);
+
+/* BaseTCSC arithmetic (comp.h:37-63) over the CSC+packed format: per column
+ * the +1 entries ascending, then the -1 entries ascending, then + b[n]. */
+void oracle_base_csc_packed(const float *X, const int32_t *col_ptr, const int32_t *row_idx,
+                            const uint8_t *packed, const float *b, float *Y, int M, int N, int K);
 
 /* Dense GEMM oracle (sparseUtils.h:92-108): y=sum_k X[m,k]*W[k,n]; Y=y+b[n]. */
 void oracle_gemm_dense(const float *X, const float *W, const float *b, float *Y, int M, int N, int K);

@@ -348,6 +348,24 @@ extern "C" int tcsc_hip_create_dense(const int32_t *W, int K, int N, int device,
     return tcsc_hip_create(csp.data(), csn.data(), rip.data(), rin.data(), K, N, device, out);
 }
 
+extern "C" int tcsc_hip_create_csc_packed(const int32_t *col_ptr, const int32_t *row_idx,
+                                          const uint8_t *packed, int K, int N, int device,
+                                          tsg_tcsc **out)
+{
+    if (!out) return fail(TSG_ERR_ARG, "null out");
+    *out = nullptr;
+    int64_t p = 0, q = 0;
+    int rc = tsg_csc_packed_to_tcsc(col_ptr, row_idx, packed, N, nullptr, nullptr, nullptr,
+                                    nullptr, &p, &q);
+    if (rc) return rc;
+    std::vector<int32_t> csp((size_t)N + 1), csn((size_t)N + 1), rip((size_t)std::max<int64_t>(p, 1)),
+        rin((size_t)std::max<int64_t>(q, 1));
+    rc = tsg_csc_packed_to_tcsc(col_ptr, row_idx, packed, N, csp.data(), csn.data(), rip.data(),
+                                rin.data(), &p, &q);
+    if (rc) return rc;
+    return tcsc_hip_create(csp.data(), csn.data(), rip.data(), rin.data(), K, N, device, out);
+}
+
 extern "C" void tcsc_hip_destroy(tsg_tcsc *h) { free_handle(h); }
 
 extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)

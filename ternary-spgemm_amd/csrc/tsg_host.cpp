@@ -325,3 +325,75 @@ extern "C" int tsg_gen_x(int64_t len, int range, uint64_t seed, float *X)
         X[i] = (float)((int64_t)tsg::below(st, 2ull * (uint64_t)range + 1) - range);
     return TSG_OK;
 }
+
+// ------------------------------------------- CSC + base-3 packed values --
+// readme.md:111: "normal CSC with compressed values vector (1s and -1s, 8
+// bits for 5 values)".  digit = v + 1, 5 digits per byte, CSC order.
+
+extern "C" int tsg_tcsc_to_csc_packed(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                                      const int32_t *rin, int N, int32_t *col_ptr,
+                                      int32_t *row_idx, uint8_t *packed, int64_t *nnz)
+{
+    if (!csp || !csn || N < 0) {
+        g_tsg_host_err = "tsg_tcsc_to_csc_packed: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    const int64_t total = (int64_t)csp[N] + (int64_t)csn[N];
+    if (nnz) *nnz = total;
+    if (total > INT32_MAX) {
+        g_tsg_host_err = "tsg_tcsc_to_csc_packed: nnz exceeds int32";
+        return TSG_ERR_RANGE;
+    }
+    if (!col_ptr || !row_idx || !packed) return TSG_OK;
+    static const int pw[5] = {1, 3, 9, 27, 81};
+    std::memset(packed, 0, (size_t)((total + 4) / 5));
+    int64_t e = 0;
+    for (int n = 0; n < N; n++) {  // merge the two ascending runs of column n
+        col_ptr[n] = (int32_t)e;
+        int32_t a = csp[n], b = csn[n];
+        while (a < csp[n + 1] || b < csn[n + 1]) {
+            const bool pos = b >= csn[n + 1] || (a < csp[n + 1] && rip[a] < rin[b]);
+            row_idx[e] = pos ? rip[a++] : rin[b++];
+            packed[e / 5] = (uint8_t)(packed[e / 5] + (pos ? 2 : 0) * pw[e % 5]);
+            e++;
+        }
+    }
+    col_ptr[N] = (int32_t)e;
+    return TSG_OK;
+}
+
+extern "C" int tsg_csc_packed_to_tcsc(const int32_t *col_ptr, const int32_t *row_idx,
+                                      const uint8_t *packed, int N, int32_t *csp, int32_t *csn,
+                                      int32_t *rip, int32_t *rin, int64_t *nnz_pos,
+                                      int64_t *nnz_neg)
+{
+    if (!col_ptr || N < 0 || col_ptr[0] != 0 || (col_ptr[N] > 0 && (!row_idx || !packed))) {
+        g_tsg_host_err = "tsg_csc_packed_to_tcsc: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    int64_t p = 0, q = 0;
+    for (int n = 0; n < N; n++) {
+        if (col_ptr[n + 1] < col_ptr[n]) {
+            g_tsg_host_err = "tsg_csc_packed_to_tcsc: col_ptr not monotone";
+            return TSG_ERR_ARG;
+        }
+        if (csp) csp[n] = (int32_t)p;
+        if (csn) csn[n] = (int32_t)q;
+        for (int32_t i = col_ptr[n]; i < col_ptr[n + 1]; i++) {
+            int d = packed[i / 5];
+            for (int j = 0; j < i % 5; j++) d /= 3;
+            d %= 3;
+            if (d == 1) {
+                g_tsg_host_err = "tsg_csc_packed_to_tcsc: stored entry with value 0 at " + std::to_string(i);
+                return TSG_ERR_ARG;
+            }
+            if (d == 2) { if (rip) rip[p] = row_idx[i]; p++; }
+            else { if (rin) rin[q] = row_idx[i]; q++; }
+        }
+    }
+    if (csp) csp[N] = (int32_t)p;
+    if (csn) csn[N] = (int32_t)q;
+    if (nnz_pos) *nnz_pos = p;
+    if (nnz_neg) *nnz_neg = q;
+    return TSG_OK;
+}

@@ -37,7 +37,8 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_gemm_dev", "tcsc_hip_gemm_prelu", "tcsc_hip_gemm_prelu_dev", "tcsc_hip_reserve",
     "tcsc_hip_info", "tcsc_hip_to_dense", "tcsc_hip_set_timing", "tcsc_hip_kernel_time",
     "tcsc_hip_last_error", "tcsc_hip_device_count", "tsg_tcsc_slice", "tsg_tcsc_validate",
-    "tsg_gen_tcsc", "tsg_gen_x",
+    "tsg_gen_tcsc", "tsg_gen_x", "tcsc_hip_create_csc_packed", "tsg_tcsc_to_csc_packed",
+    "tsg_csc_packed_to_tcsc",
 )
 
 
@@ -101,6 +102,10 @@ def lib() -> C.CDLL:
     L.tsg_gen_tcsc.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
                                vp, vp, vp, vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.tsg_gen_x.argtypes = [C.c_int64, C.c_int, C.c_uint64, vp]
+    L.tcsc_hip_create_csc_packed.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, C.POINTER(H)]
+    L.tsg_tcsc_to_csc_packed.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, vp, C.POINTER(C.c_int64)]
+    L.tsg_csc_packed_to_tcsc.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp,
+                                         C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     for f in EXPORTED_SYMBOLS:
         if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error"):
             getattr(L, f).restype = C.c_int
@@ -165,6 +170,37 @@ def gen_tcsc(K: int, N: int, s: int, seed: int, n0: int = 0, n1: Optional[int] =
     return o[0], o[1], o[2][: p.value], o[3][: q.value]
 
 
+def tcsc_to_csc_packed(csp, csn, rip, rin, N: int):
+    """TCSC -> CSC + base-3 packed values (readme.md:111)."""
+    csp, csn, rip, rin = map(_i32, (csp, csn, rip, rin))
+    nnz = C.c_int64()
+    L = lib()
+    _check(L.tsg_tcsc_to_csc_packed(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), N, None, None,
+                                    None, C.byref(nnz)), "tsg_tcsc_to_csc_packed")
+    col_ptr = np.empty(N + 1, np.int32)
+    row_idx = np.empty(max(nnz.value, 1), np.int32)
+    packed = np.empty(max((nnz.value + 4) // 5, 1), np.uint8)
+    _check(L.tsg_tcsc_to_csc_packed(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), N,
+                                    col_ptr.ctypes.data, row_idx.ctypes.data, packed.ctypes.data,
+                                    C.byref(nnz)), "tsg_tcsc_to_csc_packed")
+    return col_ptr, row_idx[: nnz.value], packed[: (nnz.value + 4) // 5]
+
+
+def csc_packed_to_tcsc(col_ptr, row_idx, packed, N: int):
+    col_ptr, row_idx = _i32(col_ptr), _i32(row_idx)
+    packed = np.ascontiguousarray(packed, dtype=np.uint8)
+    p, q = C.c_int64(), C.c_int64()
+    L = lib()
+    _check(L.tsg_csc_packed_to_tcsc(_ptr(col_ptr), _ptr(row_idx), _ptr(packed), N, None, None,
+                                    None, None, C.byref(p), C.byref(q)), "tsg_csc_packed_to_tcsc")
+    o = [np.empty(N + 1, np.int32), np.empty(N + 1, np.int32),
+         np.empty(max(p.value, 1), np.int32), np.empty(max(q.value, 1), np.int32)]
+    _check(L.tsg_csc_packed_to_tcsc(_ptr(col_ptr), _ptr(row_idx), _ptr(packed), N,
+                                    *(a.ctypes.data for a in o), C.byref(p), C.byref(q)),
+           "tsg_csc_packed_to_tcsc")
+    return o[0], o[1], o[2][: p.value], o[3][: q.value]
+
+
 def gen_x(M: int, K: int, seed: int, rng: int = 512) -> np.ndarray:
     """Integer-valued fp32 X in [-rng, rng] (initX, sparseUtils.h:6-23)."""
     X = np.empty((M, K), np.float32)
@@ -190,6 +226,20 @@ class TCSCDevice:
         _check(lib().tcsc_hip_create(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), self.K,
                                      self.N, device, C.byref(h)), "tcsc_hip_create")
         self._h = h
+
+    @classmethod
+    def from_csc_packed(cls, col_ptr, row_idx, packed, K: int, N: int,
+                        device: int = -1) -> "TCSCDevice":
+        """CSC + base-3 packed values (readme.md:111) -> same device image."""
+        col_ptr, row_idx = _i32(col_ptr), _i32(row_idx)
+        packed = np.ascontiguousarray(packed, dtype=np.uint8)
+        self = cls.__new__(cls)
+        self.K, self.N = int(K), int(N)
+        h = C.c_void_p()
+        _check(lib().tcsc_hip_create_csc_packed(_ptr(col_ptr), _ptr(row_idx), _ptr(packed), K, N,
+                                                device, C.byref(h)), "tcsc_hip_create_csc_packed")
+        self._h = h
+        return self
 
     @classmethod
     def from_dense(cls, W, device: int = -1) -> "TCSCDevice":

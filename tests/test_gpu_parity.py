@@ -189,3 +189,16 @@ def test_errors_are_loud(tsg, oracle_mod):
         tsg.TCSCDevice(t.col_start_pos, t.col_start_neg, t.row_index_pos[::-1].copy(),
                        t.row_index_neg, 64, 32)
     h(X, b, Y, 0, 32, 64)  # M = 0 is a no-op, as the reference's empty loop
+
+
+def test_csc_packed_input(tsg, oracle_mod):
+    """readme.md:111 format in, identical BaseTCSC chains out."""
+    O = oracle_mod
+    for s in (2, 4, 8, 16):
+        K, N, M = 900, 700, 130
+        W = O.gen_ternary(K, N, s, s)
+        t = O.tcsc_encode(W)
+        h = tsg.TCSCDevice.from_csc_packed(*O.csc_packed_encode(W), K, N)
+        X = O.init_x_frac(M, K, s)
+        b = np.linspace(-1, 1, N).astype(np.float32)
+        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))

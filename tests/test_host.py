@@ -106,3 +106,25 @@ def test_no_gpu_fails_loudly(tsg, oracle_mod):
     with pytest.raises(tsg.TSGError) as e:
         tsg.TCSCDevice(*t.arrays, 4, 4)
     assert e.value.code == 4  # TSG_ERR_NODEV: never a silent CPU fallback
+
+
+def test_csc_packed_conversions(tsg, oracle_mod):
+    """CSC + base-3 packed values (readme.md:111) <-> TCSC, vs the oracle encoder."""
+    O = oracle_mod
+    for K, N, s in [(300, 77, 4), (64, 5, 1), (10, 10, 16), (129, 300, 2)]:
+        W = O.gen_ternary(K, N, s, 3)
+        t = O.tcsc_encode(W)
+        ref = O.csc_packed_encode(W)
+        got = tsg.tcsc_to_csc_packed(*t.arrays, N)
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b)
+        back = tsg.csc_packed_to_tcsc(*ref, N)
+        for a, b in zip(back, t.arrays):
+            assert np.array_equal(a, b)
+        X = O.init_x_frac(3, K, 1)
+        b = np.ones(N, np.float32)
+        assert np.array_equal(O.base_csc_packed(X, *ref, b, K, N).view(np.uint32),
+                              O.base_tcsc(X, t, b).view(np.uint32))
+    # a stored entry with value 0 (digit 1) is rejected
+    with pytest.raises(tsg.TSGError):
+        tsg.csc_packed_to_tcsc(np.array([0, 1]), np.array([0]), np.array([1], np.uint8), 1)
