@@ -31,6 +31,10 @@ import tsg_dist as D  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 PROFILE_PMC = os.path.join(REPO, "profiles", "r01_pmc_summary.json")
+# LDS read roof of the stream kernel: 256 B/clk/CU (ds_read_b64, MI355X_MICROARCH.md
+# LDS table) x 256 CUs x 2.4 GHz.  Every (nonzero, 128-row tile) costs one 512-B
+# ds_read_b64 wave-instruction.
+LDS_PEAK_TBPS = 256 * 256 * 2.4e9 / 1e12
 
 
 def parse():
@@ -154,6 +158,7 @@ def main():
         value = flops_all * a.steps / elapsed_max / 1e9
         ms_step = elapsed_max / a.steps * 1e3
         alg_bytes = T.algorithmic_bytes(M, Nr, K, nnz)  # per launch, this rank
+        lds_bytes = ((M + 127) // 128) * nnz * 512       # LDS bytes the gathers must read
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
         traffic = None
         try:
@@ -185,7 +190,13 @@ def main():
                          "traffic": traffic,
                          "kernel": "tsg_tcsc_lds_kernel", "kernel_ms": round(kern_ms_max, 4),
                          "algorithmic_bytes_per_launch": alg_bytes,
-                         "kernel_gflops": round(T.flops(M, Nr, nnz) / (kern_ms_max * 1e-3) / 1e9, 2)},
+                         "kernel_gflops": round(T.flops(M, Nr, nnz) / (kern_ms_max * 1e-3) / 1e9, 2),
+                         "traffic_source": (PROFILE_PMC if traffic is not None else None),
+                         "lds": {"bound_for": "stream kernel at this M (DESIGN.md 5)",
+                                 "algorithmic_bytes": lds_bytes,
+                                 "achieved_TBps": round(lds_bytes / (kern_ms_max * 1e-3) / 1e12, 2),
+                                 "peak_TBps": round(LDS_PEAK_TBPS, 1),
+                                 "frac": round(lds_bytes / (kern_ms_max * 1e-3) / 1e12 / LDS_PEAK_TBPS, 4)}},
             "cpu_baseline": cpu,
             "stream_ms_per_step": round(stream_ms / a.steps, 4),
             "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),

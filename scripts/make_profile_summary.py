@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Turn a scripts/profile_gpu.sh output dir into the committed profile summary.
+
+  scripts/make_profile_summary.py gpurun_out/prof_<tag> profiles/<round> M K N s
+
+Writes <round>_kernel_stats.csv (rocprofv3 --stats copy), <round>_kernel_trace_tsg.csv
+(our dispatches only) and <round>_pmc_summary.json:
+  per-kernel counter totals / launch, HBM bytes corrected as MI355X_MICROARCH.md
+  (HBM section) prescribes: FETCH_SIZE is KiB and reads 1/2 of a wide (16 B/lane)
+  coalesced stream on gfx950 -> read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is
+  exact for 16-B-per-lane stores -> write bytes = WRITE_SIZE * 1024.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+M, K, N, s = (int(v) for v in sys.argv[3:7])
+os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
+stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+if stats:
+    shutil.copy(stats[0], dst + "_kernel_stats.csv")
+trace = glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))
+if trace:
+    rows = [r for r in csv.DictReader(open(trace[0])) if "tsg" in r["Kernel_Name"]]
+    if rows:
+        with open(dst + "_kernel_trace_tsg.csv", "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+            w.writeheader()
+            w.writerows(rows)
+
+tot = collections.defaultdict(lambda: collections.defaultdict(float))
+disp = collections.defaultdict(lambda: collections.defaultdict(set))
+for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"]
+        if "tsg" not in k:
+            continue
+        kn = k.split("(")[0].replace("void ", "").strip()
+        tot[kn][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[kn][r["Counter_Name"]].add(r["Dispatch_Id"])
+out = {"workload": f"{M}x{K}x{N}s{s}", "kernels": {}, "per_launch_hbm_bytes": {}}
+for kn, v in tot.items():
+    per = {c: x / max(len(disp[kn][c]), 1) for c, x in v.items()}
+    o = {"per_launch": per}
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        o["hbm_read_bytes"] = 2 * per["FETCH_SIZE"] * 1024
+        o["hbm_write_bytes"] = per["WRITE_SIZE"] * 1024
+        o["hbm_bytes"] = o["hbm_read_bytes"] + o["hbm_write_bytes"]
+    if "GRBM_GUI_ACTIVE" in per:
+        o["gpu_cycles_per_xcd"] = per["GRBM_GUI_ACTIVE"] / 8
+    if "SQ_LDS_IDX_ACTIVE" in per and "GRBM_GUI_ACTIVE" in per:
+        o["lds_util"] = per["SQ_LDS_IDX_ACTIVE"] / (per["GRBM_GUI_ACTIVE"] / 8 * 256)
+    out["kernels"][kn] = o
+    if "stream_kernel" in kn and "hbm_bytes" in o:
+        out["per_launch_hbm_bytes"][out["workload"]] = o["hbm_bytes"]
+json.dump(out, open(dst + "_pmc_summary.json", "w"), indent=1)
+print(json.dumps(out, indent=1)[:3000])
