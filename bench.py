@@ -188,7 +188,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic,
-                         "kernel": "tsg_tcsc_lds_kernel", "kernel_ms": round(kern_ms_max, 4),
+                         "kernel": "tsg_tcsc_stream_kernel", "kernel_ms": round(kern_ms_max, 4),
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "kernel_gflops": round(T.flops(M, Nr, nnz) / (kern_ms_max * 1e-3) / 1e9, 2),
                          "traffic_source": (PROFILE_PMC if traffic is not None else None),
