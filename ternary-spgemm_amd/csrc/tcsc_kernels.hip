@@ -372,6 +372,128 @@ __device__ __forceinline__ void walk_chunk(float2 (&acc)[NW], const uint32_t (&c
     }
 }
 
+// ------------------------------------------------------------ flat walk --
+// The wave's step is ONE dword stream (segments back to back).  Accumulators
+// live in a register vector indexed by the current column (hipcc lowers the
+// uniform dynamic index to s_set_gpr_idx register moves at segment
+// boundaries only).  The loop is software-pipelined by one dword pair: the
+// 8 ds_reads of pair p+1 are in flight while the adds of pair p run, so each
+// wave always keeps LDS busy; every chain still adds in stream order.
+template <int NW>
+struct AccVec {
+    typedef float type __attribute__((ext_vector_type(2 * NW)));
+};
+
+template <int NW>
+struct ColCursor {
+    uint64_t lo, hi;   // remaining per-column dword counts, 8 bits each, LSB first
+    int cur;           // current column
+    uint32_t rem;      // dwords left in the current column
+    __device__ __forceinline__ void advance()
+    {
+        do {
+            cur++;
+            rem = (uint32_t)(lo & 0xffu);
+            lo = (lo >> 8) | (hi << 56);
+            hi >>= 8;
+        } while (rem == 0 && cur < NW - 1);
+    }
+};
+
+template <int NW, bool NEG>
+__device__ __forceinline__ void flat_quad(float2 &work, const float2 (&x)[4], ColCursor<NW> &cc,
+                                          typename AccVec<NW>::type &acc)
+{
+    work = chain_step<NEG>(work, x[0]);
+    work = chain_step<NEG>(work, x[1]);
+    work = chain_step<NEG>(work, x[2]);
+    work = chain_step<NEG>(work, x[3]);
+    if (--cc.rem == 0) {  // segment boundary (wave-uniform, ~1 in 4 dwords)
+        acc[2 * cc.cur] = work.x;
+        acc[2 * cc.cur + 1] = work.y;
+        if (cc.cur < NW - 1) {
+            cc.advance();
+            work = make_float2(acc[2 * cc.cur], acc[2 * cc.cur + 1]);
+        }
+    }
+}
+
+__device__ __forceinline__ void flat_reads(float2 (&x)[4], uint32_t w, uint32_t lanec, const char *lds)
+{
+    x[0] = lds_f2(lds, entry_addr<0>(w, lanec));
+    x[1] = lds_f2(lds, entry_addr<1>(w, lanec));
+    x[2] = lds_f2(lds, entry_addr<2>(w, lanec));
+    x[3] = lds_f2(lds, entry_addr<3>(w, lanec));
+}
+
+template <int NW, bool NEG>
+__device__ __forceinline__ void flat_pair(float2 &work, const float2 (&x)[8], ColCursor<NW> &cc,
+                                          typename AccVec<NW>::type &acc)
+{
+    const float2 lo[4] = {x[0], x[1], x[2], x[3]};
+    const float2 hi[4] = {x[4], x[5], x[6], x[7]};
+    flat_quad<NW, NEG>(work, lo, cc, acc);
+    flat_quad<NW, NEG>(work, hi, cc, acc);
+}
+
+__device__ __forceinline__ void flat_reads8(float2 (&x)[8], uint2 w, uint32_t lanec, const char *lds)
+{
+    x[0] = lds_f2(lds, entry_addr<0>(w.x, lanec));
+    x[1] = lds_f2(lds, entry_addr<1>(w.x, lanec));
+    x[2] = lds_f2(lds, entry_addr<2>(w.x, lanec));
+    x[3] = lds_f2(lds, entry_addr<3>(w.x, lanec));
+    x[4] = lds_f2(lds, entry_addr<0>(w.y, lanec));
+    x[5] = lds_f2(lds, entry_addr<1>(w.y, lanec));
+    x[6] = lds_f2(lds, entry_addr<2>(w.y, lanec));
+    x[7] = lds_f2(lds, entry_addr<3>(w.y, lanec));
+}
+
+__device__ __forceinline__ uint2 idx_pair(const char *lds, uint32_t pd, uint32_t p)
+{
+    return *reinterpret_cast<const uint2 *>(lds + pd + 8u * p);  // broadcast read
+}
+
+// Pipeline.  LDS returns in order, so the index pair of dword pair p+2 is
+// fetched BEFORE the 8 data reads of pair p+1 (a later wait on it then does
+// not drain those reads); the adds of pair p run while pair p+1 is in
+// flight.  Reads past the step's data are harmless: any entry byte maps into
+// the X^T region.
+template <int NW, bool NEG>
+__device__ __forceinline__ void walk_chunk_flat(typename AccVec<NW>::type &acc, const uint32_t (&hw)[8],
+                                                uint32_t ib, uint32_t lanec, const char *lds)
+{
+    const uint32_t npairs = hw[1] >> 1;
+    if (npairs == 0) return;
+    ColCursor<NW> cc;
+    cc.lo = (uint64_t)hw[2] | ((uint64_t)hw[3] << 32);
+    cc.hi = (uint64_t)hw[4] | ((uint64_t)hw[5] << 32);
+    cc.cur = -1;
+    cc.advance();
+    float2 work = make_float2(acc[2 * cc.cur], acc[2 * cc.cur + 1]);
+    const uint32_t pd = ib + 4u * kSFlatHdrWords;
+    uint2 w = idx_pair(lds, pd, 0);
+    uint2 wn = idx_pair(lds, pd, 1);
+    float2 xa[4], xb[4];
+    flat_reads(xa, w.x, lanec, lds);
+    flat_reads(xb, w.y, lanec, lds);
+    for (uint32_t p = 1; p < npairs; p++) {
+        w = wn;
+        wn = idx_pair(lds, pd, p + 1);      // 2 pairs ahead of the adds
+        float2 ya[4], yb[4];
+        flat_reads(ya, w.x, lanec, lds);    // pair p in flight ...
+        flat_reads(yb, w.y, lanec, lds);
+        flat_quad<NW, NEG>(work, xa, cc, acc);  // ... while pair p-1 is added
+        flat_quad<NW, NEG>(work, xb, cc, acc);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            xa[i] = ya[i];
+            xb[i] = yb[i];
+        }
+    }
+    flat_quad<NW, NEG>(work, xa, cc, acc);
+    flat_quad<NW, NEG>(work, xb, cc, acc);
+}
+
 // LDS-DMA of X^T chunk j (127 rows x 128 M) into buffer `buf`: 64 pieces of
 // 1 KiB (4 rows of one half), 4 per wave; row 127 (the zero row) is sourced
 // from a zeroed global buffer so every refill also re-zeroes it.
@@ -396,7 +518,7 @@ __device__ __forceinline__ void stage_idx(const uint32_t *__restrict__ ent, uint
 
 // STAMP: diagnostic build only (TSG_STAMPS=1): per wave, s_memtime cycles
 // spent walking vs. waiting at the step barrier, written to `stamps`.
-template <int NW, bool PRELU, bool STAMP>
+template <int NW, bool PRELU, bool STAMP, bool FLAT>
 __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wstart,
     const uint32_t *__restrict__ ent, const float *__restrict__ zero, const float *__restrict__ b,
@@ -429,6 +551,7 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
     float2 acc[NW];
 #pragma unroll
     for (int c = 0; c < NW; c++) acc[c] = make_float2(0.0f, 0.0f);  // comp.h:41
+    typename AccVec<NW>::type accv = {};                            // FLAT: same, as a vector
 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -441,10 +564,11 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
 #ifndef TSG_NO_PRIO
         __builtin_amdgcn_s_setprio(3);
 #endif
-        // header of this step: [len][NW count bytes]
-        uint32_t hw[StreamHeader<NW>::kWords];
+        // header of this step: [len][NW count bytes] / FLAT: [len][D][NW dword-count bytes]
+        constexpr int kHW = FLAT ? kSFlatHdrWords : StreamHeader<NW>::kWords;
+        uint32_t hw[kHW > 8 ? kHW : 8] = {};
 #pragma unroll
-        for (int i = 0; i < StreamHeader<NW>::kWords; i += 2) {
+        for (int i = 0; i < kHW; i += 2) {
             const uint2 v = *reinterpret_cast<const uint2 *>(lds + ib + 4 * i);
             hw[i] = __builtin_amdgcn_readfirstlane(v.x);
             hw[i + 1] = __builtin_amdgcn_readfirstlane(v.y);
@@ -454,11 +578,19 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
             stage_x(XT, zero, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
             stage_idx(ent, sbase, ireg + (uint32_t)((q + 1) & 1) * kSIdxWaveBytes, lane);
         }
-        uint32_t cw[NW / 4];
+        if (FLAT) {
+            uint32_t h8[8];
 #pragma unroll
-        for (int i = 0; i < NW / 4; i++) cw[i] = hw[1 + i];
-        if (q < nch) walk_chunk<NW, false>(acc, cw, ib, lanec, lds);  // +1 runs, ascending K
-        else walk_chunk<NW, true>(acc, cw, ib, lanec, lds);           // -1 runs, ascending K
+            for (int i = 0; i < 8; i++) h8[i] = hw[i];
+            if (q < nch) walk_chunk_flat<NW, false>(accv, h8, ib, lanec, lds);  // +1 runs
+            else walk_chunk_flat<NW, true>(accv, h8, ib, lanec, lds);           // -1 runs
+        } else {
+            uint32_t cw[NW / 4];
+#pragma unroll
+            for (int i = 0; i < NW / 4; i++) cw[i] = hw[1 + i];
+            if (q < nch) walk_chunk<NW, false>(acc, cw, ib, lanec, lds);  // +1 runs, ascending K
+            else walk_chunk<NW, true>(acc, cw, ib, lanec, lds);           // -1 runs, ascending K
+        }
         if (STAMP) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             tb = __builtin_amdgcn_s_memtime();
@@ -479,6 +611,10 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
         o[3] = (unsigned long long)((nt << 16) | mt);
     }
 
+    if (FLAT) {
+#pragma unroll
+        for (int c = 0; c < NW; c++) acc[c] = make_float2(accv[2 * c], accv[2 * c + 1]);
+    }
     if (ncol0 >= N) return;
 #pragma unroll
     for (int r = 0; r < kRowsPerLane; r++) {
@@ -544,25 +680,31 @@ int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *en
 template <int NW, bool PRELU, bool STAMP>
 static void launch_stream_nw(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                              const float *zero, const float *b, const float *alpha, float *Y, int M,
-                             int N, int Npad, int nch, unsigned long long *stamps, hipStream_t s)
+                             int N, int Npad, int nch, unsigned long long *stamps, bool flat,
+                             hipStream_t s)
 {
     const int mtiles = Mp / kTileM, ntiles = Npad / (kSWaves * NW);
-    hipLaunchKernelGGL((tsg_tcsc_stream_kernel<NW, PRELU, STAMP>), dim3((unsigned)(mtiles * ntiles)),
-                       dim3(1024), 0, s, XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, nch, mtiles,
-                       ntiles, stamps);
+    if (flat)
+        hipLaunchKernelGGL((tsg_tcsc_stream_kernel<NW, PRELU, STAMP, true>),
+                           dim3((unsigned)(mtiles * ntiles)), dim3(1024), 0, s, XT, Mp, wstart, ent,
+                           zero, b, alpha, Y, M, N, nch, mtiles, ntiles, stamps);
+    else
+        hipLaunchKernelGGL((tsg_tcsc_stream_kernel<NW, PRELU, STAMP, false>),
+                           dim3((unsigned)(mtiles * ntiles)), dim3(1024), 0, s, XT, Mp, wstart, ent,
+                           zero, b, alpha, Y, M, N, nch, mtiles, ntiles, stamps);
 }
 
 int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                        const float *zero, const float *b, const float *alpha, float *Y, int M,
                        int N, int Npad, int nch, int nw, int prelu, unsigned long long *stamps,
-                       void *stream)
+                       bool flat, void *stream)
 {
     hipStream_t s = (hipStream_t)stream;
 #define TSG_NW(NWV)                                                                               \
     if (nw == NWV) {                                                                              \
-        if (stamps) launch_stream_nw<NWV, false, true>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, stamps, s); \
-        else if (prelu) launch_stream_nw<NWV, true, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, nullptr, s); \
-        else launch_stream_nw<NWV, false, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, nullptr, s); \
+        if (stamps) launch_stream_nw<NWV, false, true>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, stamps, flat, s); \
+        else if (prelu) launch_stream_nw<NWV, true, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, nullptr, flat, s); \
+        else launch_stream_nw<NWV, false, false>(XT, Mp, wstart, ent, zero, b, alpha, Y, M, N, Npad, nch, nullptr, flat, s); \
         return hipGetLastError() == hipSuccess ? 0 : -1;                                          \
     }
     TSG_NW(16)

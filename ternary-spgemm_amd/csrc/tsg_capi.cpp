@@ -31,7 +31,7 @@ static int fail(int code, const std::string &msg)
 struct tsg_tcsc {
     int K = 0, N = 0, device = 0;
     int64_t nnz_pos = 0, nnz_neg = 0;
-    bool stream_kernel = true;            // TSG_KERNEL=chunked selects the round-1 v1 kernel
+    bool stream_kernel = true;            // TSG_KERNEL=chunked: v1 kernel; =flat: flat-stream variant
     tsg::Image img;                       // v1 device image (chunked kernel)
     tsg::StreamImage simg;                // device image of the stream kernel
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
@@ -167,7 +167,8 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     const int lrc = h->stream_kernel
         ? tsg::launch_tcsc_stream(h->d_work, Mp, h->d_seg, h->d_ent, h->d_zero, db, dalpha, dY, M, N,
-                                  h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, stamps, s)
+                                  h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, stamps,
+                                  h->simg.flat, s)
         : tsg::launch_tcsc(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->img.Npad,
                            h->img.nch, h->img.tile_cols, prelu ? 1 : 0, s);
     if (lrc != 0)
@@ -297,7 +298,8 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     h->stream_kernel = !(kenv && std::strcmp(kenv, "chunked") == 0);
     const std::vector<uint32_t> *segv, *entv;
     if (h->stream_kernel) {
-        tsg::plan_stream_image(csp, csn, rip, rin, K, N, h->simg);
+        tsg::plan_stream_image(csp, csn, rip, rin, K, N, kenv && std::strcmp(kenv, "flat") == 0,
+                               h->simg);
         segv = &h->simg.wstart;
         entv = &h->simg.ent;
     } else {

@@ -65,16 +65,17 @@ void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 }
 
 int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, int nw, StreamImage &img)
+                       const int32_t *rin, int K, int N, int nw, bool flat, StreamImage &img)
 {
     img.K = K;
     img.N = N;
     img.nw = nw;
+    img.flat = flat;
     img.tile_cols = kSWaves * nw;
     img.Npad = ((N + img.tile_cols - 1) / img.tile_cols) * img.tile_cols;
     img.nch = std::max(1, (K + kSChunk - 1) / kSChunk);
     const int nch = img.nch, ntiles = img.Npad / img.tile_cols;
-    const int hdr_words = ((1 + nw / kEntPerWord) + 1) & ~1;
+    const int hdr_words = flat ? kSFlatHdrWords : ((1 + nw / kEntPerWord) + 1) & ~1;
     img.wstart.assign((size_t)ntiles * kSWaves, 0u);
     img.ent.clear();
     const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
@@ -101,8 +102,10 @@ int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
                 align(4);  // sub-stream: 16-byte aligned for the LDS-DMA piece
                 const size_t sub0 = img.ent.size();
                 img.ent.resize(sub0 + hdr_words, 0u);
+                int last_nonempty = -1;
                 for (int c = 0; c < nw; c++) {
-                    align(2);  // segment: 8-byte aligned for ds_read_b64
+                    if (!flat) align(2);  // segment: 8-byte aligned for ds_read_b64
+                    const size_t seg0 = img.ent.size();
                     const int n = n0 + c;
                     int32_t &i = cur[(size_t)c * 2 + p];
                     const int32_t e = n < N ? cs[n + 1] : 0;
@@ -124,8 +127,24 @@ int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
                             word |= ((uint32_t)kSZeroRow | par) << (8 * fill);
                         img.ent.push_back(word);
                     }
-                    // exact entry count (<= kSChunk): the kernel reads no padding
-                    img.ent[sub0 + 1 + c / kEntPerWord] |= nent << (8 * (c % kEntPerWord));
+                    if (flat) {  // dwords of the segment; segments follow each other
+                        const uint32_t dw = (uint32_t)(img.ent.size() - seg0);
+                        img.ent[sub0 + 2 + c / kEntPerWord] |= dw << (8 * (c % kEntPerWord));
+                        if (dw) last_nonempty = c;
+                    } else {  // exact entry count (<= kSChunk)
+                        img.ent[sub0 + 1 + c / kEntPerWord] |= nent << (8 * (c % kEntPerWord));
+                    }
+                }
+                if (flat) {
+                    size_t D = img.ent.size() - sub0 - hdr_words;
+                    if (D & 1) {  // even: the kernel walks dword pairs; the extra dword of
+                        // +0.0f-row entries joins the last non-empty segment
+                        img.ent.push_back(0x01010101u * ((uint32_t)kSZeroRow | par));
+                        const int c = last_nonempty;
+                        img.ent[sub0 + 2 + c / kEntPerWord] += 1u << (8 * (c % kEntPerWord));
+                        D++;
+                    }
+                    img.ent[sub0 + 1] = (uint32_t)D;
                 }
                 align(4);  // len is the exact distance to the next sub-stream
                 const size_t len = img.ent.size() - sub0;
@@ -140,13 +159,13 @@ int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
 }
 
 void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, StreamImage &img)
+                       const int32_t *rin, int K, int N, bool flat, StreamImage &img)
 {
     for (int nw : {16, 8}) {
         if (nw == 16 && N <= kSWaves * 8) continue;  // tiny N: narrower tiles waste less
-        if (build_stream_image(csp, csn, rip, rin, K, N, nw, img) <= kSSubMax) return;
+        if (build_stream_image(csp, csn, rip, rin, K, N, nw, flat, img) <= kSSubMax) return;
     }
-    build_stream_image(csp, csn, rip, rin, K, N, 4, img);  // 2 + 4*32 dwords always fit
+    build_stream_image(csp, csn, rip, rin, K, N, 4, flat, img);  // 8 + 4*32+1 dwords always fit
 }
 
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,

@@ -39,8 +39,16 @@ constexpr int kSSubMax = kSIdxWaveBytes / 4;             // max dwords of one st
 // (k - j*kSChunk) | (q&1)<<7, ascending k, 4 per dword, the last dword padded
 // with kSZeroRow | (q&1)<<7.  A sub-stream is at most kSSubMax dwords; the
 // planner lowers nw (16 -> 8 -> 4) until that holds.
+// Flat variant (default, tsg_tcsc_flat_kernel): the header is 8 dwords
+// [len][D = data dwords, even][NW bytes = dwords of each column segment]...,
+// data at +32 B, segments back to back (no per-segment alignment), every
+// segment padded to whole dwords with +0.0f-row entries, and one more such
+// dword appended to the last non-empty segment when D would be odd.
+constexpr int kSFlatHdrWords = 8;
+
 struct StreamImage {
     int K = 0, N = 0, Npad = 0, nch = 0;
+    bool flat = true;
     int nw = 0;                     // columns per wave
     int tile_cols = 0;              // kSWaves * nw
     std::vector<uint32_t> wstart;   // per (column tile, wave): first dword of its stream
@@ -49,10 +57,10 @@ struct StreamImage {
 // Returns the largest sub-stream (dwords); callers retry with a smaller nw
 // when it exceeds kSSubMax.
 int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, int nw, StreamImage &img);
+                       const int32_t *rin, int K, int N, int nw, bool flat, StreamImage &img);
 // Builds with the widest nw (16, 8, 4) whose sub-streams fit.
 void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, StreamImage &img);
+                       const int32_t *rin, int K, int N, bool flat, StreamImage &img);
 
 // ---------------------------------------------------------------------------
 // "chunked" kernel (tsg_tcsc_lds_kernel, round-1 v1, kept for A/B)
@@ -81,6 +89,6 @@ int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *en
 int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                        const float *zero, const float *b, const float *alpha, float *Y, int M,
                        int N, int Npad, int nch, int nw, int prelu, unsigned long long *stamps,
-                       void *stream);
+                       bool flat, void *stream);
 
 }  // namespace tsg
