@@ -270,6 +270,7 @@ __device__ __forceinline__ float2 walk_column(float2 a, uint32_t ipos, uint32_t 
             a = chain_step<NEG>(a, x6);
             a = chain_step<NEG>(a, x7);
             w = nx;
+            asm volatile("" ::: "memory");  // keep the prefetch (see walk_pair)
         }
     }
     if (i < full) {
@@ -287,6 +288,48 @@ __device__ __forceinline__ float2 walk_column(float2 a, uint32_t ipos, uint32_t 
 // Two columns walked in lockstep for min(ca, cb) dwords: two independent
 // chains per wave interleave their LDS latency; each chain keeps its own
 // order.  The longer column finishes alone.
+//
+// Software pipeline (default; -DTSG_NO_PIPE for the plain loop): the 8 reads
+// of the next dword are in flight while the current dword's 8 adds run, and
+// the index words of the next 2-dword block are read BEFORE those data reads
+// (LDS returns in order, so waiting for them never drains the data in
+// flight).  sched_barrier pins that issue order against the scheduler.
+#ifdef TSG_NO_PIPE
+constexpr bool kPipe = false;
+#else
+constexpr bool kPipe = true;
+#endif
+
+struct Quad2 { float2 a[4], b[4]; };
+
+__device__ __forceinline__ void pair_reads(Quad2 &q, uint32_t wa, uint32_t wb, uint32_t lanec,
+                                           const char *lds)
+{
+    q.a[0] = lds_f2(lds, entry_addr<0>(wa, lanec));
+    q.b[0] = lds_f2(lds, entry_addr<0>(wb, lanec));
+    q.a[1] = lds_f2(lds, entry_addr<1>(wa, lanec));
+    q.b[1] = lds_f2(lds, entry_addr<1>(wb, lanec));
+    q.a[2] = lds_f2(lds, entry_addr<2>(wa, lanec));
+    q.b[2] = lds_f2(lds, entry_addr<2>(wb, lanec));
+    q.a[3] = lds_f2(lds, entry_addr<3>(wa, lanec));
+    q.b[3] = lds_f2(lds, entry_addr<3>(wb, lanec));
+}
+
+template <bool NEG>
+__device__ __forceinline__ void pair_adds(float2 &a, float2 &b, const Quad2 &q)
+{
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        a = chain_step<NEG>(a, q.a[e]);
+        b = chain_step<NEG>(b, q.b[e]);
+    }
+}
+
+__device__ __forceinline__ uint2 lds_u2(const char *lds, uint32_t a)
+{
+    return *reinterpret_cast<const uint2 *>(lds + a);
+}
+
 template <bool NEG>
 __device__ __forceinline__ void walk_pair(float2 &acc_a, float2 &acc_b, uint32_t pa, uint32_t ea,
                                           uint32_t pb, uint32_t eb, uint32_t lanec, const char *lds)
@@ -295,44 +338,44 @@ __device__ __forceinline__ void walk_pair(float2 &acc_a, float2 &acc_b, uint32_t
     const uint32_t joint = ca < cb ? ca : cb;
     float2 a = acc_a, b = acc_b;
     uint32_t i = 0;
-    if (joint >= 2) {
-        uint2 wa = *reinterpret_cast<const uint2 *>(lds + pa);
-        uint2 wb = *reinterpret_cast<const uint2 *>(lds + pb);
+    if (kPipe) {
+        const uint32_t nblk = joint >> 1;
+        if (nblk) {
+            uint2 wa = lds_u2(lds, pa), wb = lds_u2(lds, pb);
+            Quad2 qa, qb;
+            pair_reads(qa, wa.x, wb.x, lanec, lds);
+            // branch-free body (a mid-loop exit gets tail-merged with the
+            // adds, which then need lgkmcnt(0) and register copies)
+            for (uint32_t blk = 1; blk < nblk; blk++) {
+                const uint2 na = lds_u2(lds, pa + 8u * blk), nb = lds_u2(lds, pb + 8u * blk);
+                __builtin_amdgcn_sched_barrier(0);
+                pair_reads(qb, wa.y, wb.y, lanec, lds);
+                __builtin_amdgcn_sched_barrier(0);
+                pair_adds<NEG>(a, b, qa);
+                __builtin_amdgcn_sched_barrier(0);
+                pair_reads(qa, na.x, nb.x, lanec, lds);
+                __builtin_amdgcn_sched_barrier(0);
+                pair_adds<NEG>(a, b, qb);
+                __builtin_amdgcn_sched_barrier(0);
+                wa = na;
+                wb = nb;
+            }
+            pair_reads(qb, wa.y, wb.y, lanec, lds);
+            pair_adds<NEG>(a, b, qa);
+            pair_adds<NEG>(a, b, qb);
+            i = 2 * nblk;
+        }
+    } else if (joint >= 2) {
+        uint2 wa = lds_u2(lds, pa);
+        uint2 wb = lds_u2(lds, pb);
         for (; i + 2 <= joint; i += 2) {
-            const uint2 na = *reinterpret_cast<const uint2 *>(lds + pa + 4 * (i + 2));
-            const uint2 nb = *reinterpret_cast<const uint2 *>(lds + pb + 4 * (i + 2));
-            const float2 x0 = lds_f2(lds, entry_addr<0>(wa.x, lanec));
-            const float2 y0 = lds_f2(lds, entry_addr<0>(wb.x, lanec));
-            const float2 x1 = lds_f2(lds, entry_addr<1>(wa.x, lanec));
-            const float2 y1 = lds_f2(lds, entry_addr<1>(wb.x, lanec));
-            const float2 x2 = lds_f2(lds, entry_addr<2>(wa.x, lanec));
-            const float2 y2 = lds_f2(lds, entry_addr<2>(wb.x, lanec));
-            const float2 x3 = lds_f2(lds, entry_addr<3>(wa.x, lanec));
-            const float2 y3 = lds_f2(lds, entry_addr<3>(wb.x, lanec));
-            const float2 x4 = lds_f2(lds, entry_addr<0>(wa.y, lanec));
-            const float2 y4 = lds_f2(lds, entry_addr<0>(wb.y, lanec));
-            const float2 x5 = lds_f2(lds, entry_addr<1>(wa.y, lanec));
-            const float2 y5 = lds_f2(lds, entry_addr<1>(wb.y, lanec));
-            const float2 x6 = lds_f2(lds, entry_addr<2>(wa.y, lanec));
-            const float2 y6 = lds_f2(lds, entry_addr<2>(wb.y, lanec));
-            const float2 x7 = lds_f2(lds, entry_addr<3>(wa.y, lanec));
-            const float2 y7 = lds_f2(lds, entry_addr<3>(wb.y, lanec));
-            a = chain_step<NEG>(a, x0);
-            b = chain_step<NEG>(b, y0);
-            a = chain_step<NEG>(a, x1);
-            b = chain_step<NEG>(b, y1);
-            a = chain_step<NEG>(a, x2);
-            b = chain_step<NEG>(b, y2);
-            a = chain_step<NEG>(a, x3);
-            b = chain_step<NEG>(b, y3);
-            a = chain_step<NEG>(a, x4);
-            b = chain_step<NEG>(b, y4);
-            a = chain_step<NEG>(a, x5);
-            b = chain_step<NEG>(b, y5);
-            a = chain_step<NEG>(a, x6);
-            b = chain_step<NEG>(b, y6);
-            a = chain_step<NEG>(a, x7);
-            b = chain_step<NEG>(b, y7);
+            const uint2 na = lds_u2(lds, pa + 4 * (i + 2));
+            const uint2 nb = lds_u2(lds, pb + 4 * (i + 2));
+            Quad2 q0, q1;
+            pair_reads(q0, wa.x, wb.x, lanec, lds);
+            pair_reads(q1, wa.y, wb.y, lanec, lds);
+            pair_adds<NEG>(a, b, q0);
+            pair_adds<NEG>(a, b, q1);
             wa = na;
             wb = nb;
         }
@@ -373,125 +416,199 @@ __device__ __forceinline__ void walk_chunk(float2 (&acc)[NW], const uint32_t (&c
 }
 
 // ------------------------------------------------------------ flat walk --
-// The wave's step is ONE dword stream (segments back to back).  Accumulators
-// live in a register vector indexed by the current column (hipcc lowers the
-// uniform dynamic index to s_set_gpr_idx register moves at segment
-// boundaries only).  The loop is software-pipelined by one dword pair: the
-// 8 ds_reads of pair p+1 are in flight while the adds of pair p run, so each
-// wave always keeps LDS busy; every chain still adds in stream order.
+// The wave's step is ONE dword stream: the column segments back to back, D
+// dwords (a multiple of 4), per-column dword counts in the header.  The walk
+// is a hand-scheduled software pipeline in inline asm (the compiler's
+// scheduler and register allocator otherwise re-serialise it: see
+// DESIGN.md, perf log):
+//   * the 4 reads of dword d+3 are issued before the 4 adds of dword d, so
+//     every wave keeps 12 LDS reads in flight through the whole step, across
+//     column boundaries;
+//   * index words come 4 at a time (ds_read_b128, broadcast) one batch ahead,
+//     issued after the data reads they must not delay; every wait is one
+//     counted lgkmcnt(13) (LDS returns in order);
+//   * the chain being extended lives in v[50:51]; at a segment boundary
+//     (a SALU counter carries out) it is written back to the accumulator
+//     vector and the next column's accumulator fetched with
+//     s_set_gpr_idx relative moves: the adds never branch.
+// Every chain still adds its entries in stream order (BaseTCSC order).
+// Fixed registers: v50-v95 (work, addresses, index batches, 4 data slots),
+// the accumulators at the top of the VGPR file, counts in s[88:91].
 template <int NW>
 struct AccVec {
     typedef float type __attribute__((ext_vector_type(2 * NW)));
 };
+typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
 
-template <int NW>
-struct ColCursor {
-    uint64_t lo, hi;   // remaining per-column dword counts, 8 bits each, LSB first
-    int cur;           // current column
-    uint32_t rem;      // dwords left in the current column
-    __device__ __forceinline__ void advance()
-    {
-        do {
-            cur++;
-            rem = (uint32_t)(lo & 0xffu);
-            lo = (lo >> 8) | (hi << 56);
-            hi >>= 8;
-        } while (rem == 0 && cur < NW - 1);
-    }
-};
+#define TSG_S0_0 "v[64:65]"
+#define TSG_S0_1 "v[66:67]"
+#define TSG_S0_2 "v[68:69]"
+#define TSG_S0_3 "v[70:71]"
+#define TSG_S1_0 "v[72:73]"
+#define TSG_S1_1 "v[74:75]"
+#define TSG_S1_2 "v[76:77]"
+#define TSG_S1_3 "v[78:79]"
+#define TSG_S2_0 "v[80:81]"
+#define TSG_S2_1 "v[82:83]"
+#define TSG_S2_2 "v[84:85]"
+#define TSG_S2_3 "v[86:87]"
+#define TSG_S3_0 "v[88:89]"
+#define TSG_S3_1 "v[90:91]"
+#define TSG_S3_2 "v[92:93]"
+#define TSG_S3_3 "v[94:95]"
 
-template <int NW, bool NEG>
-__device__ __forceinline__ void flat_quad(float2 &work, const float2 (&x)[4], ColCursor<NW> &cc,
-                                          typename AccVec<NW>::type &acc)
-{
-    work = chain_step<NEG>(work, x[0]);
-    work = chain_step<NEG>(work, x[1]);
-    work = chain_step<NEG>(work, x[2]);
-    work = chain_step<NEG>(work, x[3]);
-    if (--cc.rem == 0) {  // segment boundary (wave-uniform, ~1 in 4 dwords)
-        acc[2 * cc.cur] = work.x;
-        acc[2 * cc.cur + 1] = work.y;
-        if (cc.cur < NW - 1) {
-            cc.advance();
-            work = make_float2(acc[2 * cc.cur], acc[2 * cc.cur + 1]);
-        }
-    }
-}
+// 4 entry addresses of index word I, 4 reads into data slot K
+#define TSG_READS(I, K)                                                        \
+    "v_perm_b32 v52, " I ", %[lanec], %[s0]\n"                                 \
+    "v_perm_b32 v53, " I ", %[lanec], %[s1]\n"                                 \
+    "v_perm_b32 v54, " I ", %[lanec], %[s2]\n"                                 \
+    "v_perm_b32 v55, " I ", %[lanec], %[s3]\n"                                 \
+    "ds_read_b64 " TSG_S##K##_0 ", v52\n"                                      \
+    "ds_read_b64 " TSG_S##K##_1 ", v53\n"                                      \
+    "ds_read_b64 " TSG_S##K##_2 ", v54\n"                                      \
+    "ds_read_b64 " TSG_S##K##_3 ", v55\n"
 
-__device__ __forceinline__ void flat_reads(float2 (&x)[4], uint32_t w, uint32_t lanec, const char *lds)
-{
-    x[0] = lds_f2(lds, entry_addr<0>(w, lanec));
-    x[1] = lds_f2(lds, entry_addr<1>(w, lanec));
-    x[2] = lds_f2(lds, entry_addr<2>(w, lanec));
-    x[3] = lds_f2(lds, entry_addr<3>(w, lanec));
-}
+// wait for slot K (13 younger LDS ops may stay in flight), 4 chained adds
+#define TSG_ADDS(NEGM, K)                                                      \
+    "s_waitcnt lgkmcnt(13)\n"                                                  \
+    "v_pk_add_f32 v[50:51], v[50:51], " TSG_S##K##_0 NEGM "\n"                 \
+    "v_pk_add_f32 v[50:51], v[50:51], " TSG_S##K##_1 NEGM "\n"                 \
+    "v_pk_add_f32 v[50:51], v[50:51], " TSG_S##K##_2 NEGM "\n"                 \
+    "v_pk_add_f32 v[50:51], v[50:51], " TSG_S##K##_3 NEGM "\n"
 
-template <int NW, bool NEG>
-__device__ __forceinline__ void flat_pair(float2 &work, const float2 (&x)[8], ColCursor<NW> &cc,
-                                          typename AccVec<NW>::type &acc)
-{
-    const float2 lo[4] = {x[0], x[1], x[2], x[3]};
-    const float2 hi[4] = {x[4], x[5], x[6], x[7]};
-    flat_quad<NW, NEG>(work, lo, cc, acc);
-    flat_quad<NW, NEG>(work, hi, cc, acc);
-}
+// one dword: reads of d+3 into slot RS, optional index batch, adds of d
+// from slot AS, boundary check (branch to the out-of-line stub T)
+#define TSG_STEP(T, I, RS, IDXOP, NEGM, AS)                                    \
+    TSG_READS(I, RS) IDXOP TSG_ADDS(NEGM, AS)                                  \
+    "s_add_u32 %[nrem], %[nrem], 1\n"                                          \
+    "s_cbranch_scc1 .Lb" #T "_%=\n"                                            \
+    ".Lr" #T "_%=:\n"
 
-__device__ __forceinline__ void flat_reads8(float2 (&x)[8], uint2 w, uint32_t lanec, const char *lds)
-{
-    x[0] = lds_f2(lds, entry_addr<0>(w.x, lanec));
-    x[1] = lds_f2(lds, entry_addr<1>(w.x, lanec));
-    x[2] = lds_f2(lds, entry_addr<2>(w.x, lanec));
-    x[3] = lds_f2(lds, entry_addr<3>(w.x, lanec));
-    x[4] = lds_f2(lds, entry_addr<0>(w.y, lanec));
-    x[5] = lds_f2(lds, entry_addr<1>(w.y, lanec));
-    x[6] = lds_f2(lds, entry_addr<2>(w.y, lanec));
-    x[7] = lds_f2(lds, entry_addr<3>(w.y, lanec));
-}
+#define TSG_ADVANCE                                                            \
+    "s_add_u32 %[cur], %[cur], 1\n"                                            \
+    "s_lshr_b64 s[88:89], s[88:89], 8\n"                                       \
+    "s_lshl_b32 %[t], s90, 24\n"                                               \
+    "s_or_b32 s89, s89, %[t]\n"                                                \
+    "s_lshr_b64 s[90:91], s[90:91], 8\n"                                       \
+    "s_and_b32 %[t], s88, 0xff\n"
 
-__device__ __forceinline__ uint2 idx_pair(const char *lds, uint32_t pd, uint32_t p)
-{
-    return *reinterpret_cast<const uint2 *>(lds + pd + 8u * p);  // broadcast read
-}
+// segment boundary after step T: write the chain back (column `own`), find
+// the next non-empty column, fetch its accumulator (s_set_gpr_idx relative
+// moves).  Past the last column the counter is parked (never carries
+// again) and `own` keeps the finished column, so the final write-back
+// repeats the same value.
+#define TSG_PUT(ACC0, ACC1)                                                    \
+    "s_set_gpr_idx_on %[own], gpr_idx(DST)\n"                                  \
+    "v_mov_b32 " ACC0 ", v50\n"                                                \
+    "v_mov_b32 " ACC1 ", v51\n"                                                \
+    "s_set_gpr_idx_off\n"
+#define TSG_GET(ACC0, ACC1)                                                    \
+    "s_lshl_b32 %[own], %[cur], 1\n"                                           \
+    "s_set_gpr_idx_on %[own], gpr_idx(SRC0)\n"                                 \
+    "v_mov_b32 v50, " ACC0 "\n"                                                \
+    "v_mov_b32 v51, " ACC1 "\n"                                                \
+    "s_set_gpr_idx_off\n"
+#define TSG_STUB(T, ACC0, ACC1, NWM1)                                          \
+    ".Lb" #T "_%=:\n"                                                          \
+    TSG_PUT(ACC0, ACC1)                                                        \
+    ".La" #T "_%=:\n"                                                          \
+    "s_cmp_ge_u32 %[cur], " NWM1 "\n"                                          \
+    "s_cbranch_scc1 .Lx" #T "_%=\n"                                            \
+    TSG_ADVANCE                                                                \
+    "s_cmp_eq_u32 %[t], 0\n"                                                   \
+    "s_cbranch_scc1 .La" #T "_%=\n"                                            \
+    "s_sub_u32 %[nrem], 0, %[t]\n"                                             \
+    TSG_GET(ACC0, ACC1)                                                        \
+    "s_branch .Lr" #T "_%=\n"                                                  \
+    ".Lx" #T "_%=:\n"                                                          \
+    "s_brev_b32 %[nrem], 1\n"                                                  \
+    "s_branch .Lr" #T "_%=\n"
 
-// Pipeline.  LDS returns in order, so the index pair of dword pair p+2 is
-// fetched BEFORE the 8 data reads of pair p+1 (a later wait on it then does
-// not drain those reads); the adds of pair p run while pair p+1 is in
-// flight.  Reads past the step's data are harmless: any entry byte maps into
-// the X^T region.
+#define TSG_IDX_A "ds_read_b128 v[56:59], %[vidx] offset:32\n"
+#define TSG_IDX_B "ds_read_b128 v[60:63], %[vidx] offset:48\n"
+
+#define TSG_FLAT_ASM(NEGM, ACC0, ACC1, NWM1)                                   \
+    "s_mov_b32 %[m0s], m0\n"                                                   \
+    "s_mov_b32 %[cur], 0\n"                                                    \
+    "s_and_b32 %[t], s88, 0xff\n"                                              \
+    "s_cmp_eq_u32 %[t], 0\n"                                                   \
+    "s_cbranch_scc0 .Li_%=\n"                                                  \
+    ".Lia_%=:\n" TSG_ADVANCE                                                   \
+    "s_cmp_eq_u32 %[t], 0\n"                                                   \
+    "s_cbranch_scc1 .Lia_%=\n"                                                 \
+    ".Li_%=:\n"                                                                \
+    "s_sub_u32 %[nrem], 0, %[t]\n"                                             \
+    TSG_GET(ACC0, ACC1)                                                        \
+    "ds_read_b128 v[56:59], %[vidx]\n"                                         \
+    "ds_read_b128 v[60:63], %[vidx] offset:16\n"                               \
+    "s_waitcnt lgkmcnt(0)\n"                                                   \
+    TSG_READS("v56", 0) TSG_READS("v57", 1)                    \
+    TSG_READS("v58", 2)                                                \
+    ".Lloop_%=:\n"                                                             \
+    TSG_STEP(0, "v59", 3, TSG_IDX_A, NEGM, 0)                  \
+    TSG_STEP(1, "v60", 0, "", NEGM, 1)                         \
+    TSG_STEP(2, "v61", 1, "", NEGM, 2)                         \
+    TSG_STEP(3, "v62", 2, "", NEGM, 3)                         \
+    "s_cmp_le_i32 %[left], 4\n"                                                \
+    "s_cbranch_scc1 .Lexit_%=\n"                                               \
+    TSG_STEP(4, "v63", 3, TSG_IDX_B, NEGM, 0)                  \
+    TSG_STEP(5, "v56", 0, "", NEGM, 1)                         \
+    TSG_STEP(6, "v57", 1, "", NEGM, 2)                         \
+    TSG_STEP(7, "v58", 2, "", NEGM, 3)                         \
+    "v_add_u32 %[vidx], 32, %[vidx]\n"                                         \
+    "s_sub_u32 %[left], %[left], 8\n"                                          \
+    "s_cmp_gt_i32 %[left], 0\n"                                                \
+    "s_cbranch_scc1 .Lloop_%=\n"                                               \
+    ".Lexit_%=:\n"                                                             \
+    "s_waitcnt lgkmcnt(0)\n"                                                   \
+    TSG_PUT(ACC0, ACC1)                                                        \
+    "s_branch .Lend_%=\n"                                                      \
+    TSG_STUB(0, ACC0, ACC1, NWM1) TSG_STUB(1, ACC0, ACC1, NWM1)                \
+    TSG_STUB(2, ACC0, ACC1, NWM1) TSG_STUB(3, ACC0, ACC1, NWM1)                \
+    TSG_STUB(4, ACC0, ACC1, NWM1) TSG_STUB(5, ACC0, ACC1, NWM1)                \
+    TSG_STUB(6, ACC0, ACC1, NWM1) TSG_STUB(7, ACC0, ACC1, NWM1)                \
+    ".Lend_%=:\n"                                                               \
+    "s_mov_b32 m0, %[m0s]\n"
+
+#define TSG_NEG_MOD " neg_lo:[0,1] neg_hi:[0,1]"
+
+#define TSG_FLAT_CLOBBERS                                                      \
+    "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59",      \
+    "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69",      \
+    "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79",      \
+    "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89",      \
+    "v90", "v91", "v92", "v93", "v94", "v95", "scc", "memory"
+
+#define TSG_FLAT_CALL(NEGM, ACCC, ACC0, ACC1, NWM1)                            \
+    asm volatile(TSG_FLAT_ASM(NEGM, ACC0, ACC1, NWM1)                          \
+                 : [acc] ACCC(acc), [cnt] "+{s[88:91]}"(cnt), [vidx] "+v"(vidx), \
+                   [cur] "=&s"(cur), [nrem] "=&s"(nrem), [t] "=&s"(t), [own] "=&s"(own), [m0s] "=&s"(m0s), \
+                   [left] "+s"(left)                                           \
+                 : [lanec] "v"(lanec), [s0] "s"(0x0C020400u | (4u << 8)),      \
+                   [s1] "s"(0x0C020400u | (5u << 8)), [s2] "s"(0x0C020400u | (6u << 8)), \
+                   [s3] "s"(0x0C020400u | (7u << 8))                           \
+                 : TSG_FLAT_CLOBBERS)
+
 template <int NW, bool NEG>
 __device__ __forceinline__ void walk_chunk_flat(typename AccVec<NW>::type &acc, const uint32_t (&hw)[8],
-                                                uint32_t ib, uint32_t lanec, const char *lds)
+                                                uint32_t ib, uint32_t lanec)
 {
-    const uint32_t npairs = hw[1] >> 1;
-    if (npairs == 0) return;
-    ColCursor<NW> cc;
-    cc.lo = (uint64_t)hw[2] | ((uint64_t)hw[3] << 32);
-    cc.hi = (uint64_t)hw[4] | ((uint64_t)hw[5] << 32);
-    cc.cur = -1;
-    cc.advance();
-    float2 work = make_float2(acc[2 * cc.cur], acc[2 * cc.cur + 1]);
-    const uint32_t pd = ib + 4u * kSFlatHdrWords;
-    uint2 w = idx_pair(lds, pd, 0);
-    uint2 wn = idx_pair(lds, pd, 1);
-    float2 xa[4], xb[4];
-    flat_reads(xa, w.x, lanec, lds);
-    flat_reads(xb, w.y, lanec, lds);
-    for (uint32_t p = 1; p < npairs; p++) {
-        w = wn;
-        wn = idx_pair(lds, pd, p + 1);      // 2 pairs ahead of the adds
-        float2 ya[4], yb[4];
-        flat_reads(ya, w.x, lanec, lds);    // pair p in flight ...
-        flat_reads(yb, w.y, lanec, lds);
-        flat_quad<NW, NEG>(work, xa, cc, acc);  // ... while pair p-1 is added
-        flat_quad<NW, NEG>(work, xb, cc, acc);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            xa[i] = ya[i];
-            xb[i] = yb[i];
-        }
+    uint32_t left = hw[1];  // D, a multiple of 4
+    if (left == 0) return;
+    U32x4 cnt = {hw[2], hw[3], hw[4], hw[5]};
+    uint32_t vidx = ib + 4u * kSFlatHdrWords;
+    uint32_t cur, nrem, t, own, m0s;  // m0s: M0 (gpr_idx state) saved around
+    if constexpr (NW == 16) {
+        if constexpr (NEG) TSG_FLAT_CALL(TSG_NEG_MOD, "+{v[96:127]}", "v96", "v97", "15");
+        else TSG_FLAT_CALL("", "+{v[96:127]}", "v96", "v97", "15");
+    } else if constexpr (NW == 8) {
+        if constexpr (NEG) TSG_FLAT_CALL(TSG_NEG_MOD, "+{v[112:127]}", "v112", "v113", "7");
+        else TSG_FLAT_CALL("", "+{v[112:127]}", "v112", "v113", "7");
+    } else {
+        static_assert(NW == 4, "NW");
+        if constexpr (NEG) TSG_FLAT_CALL(TSG_NEG_MOD, "+{v[120:127]}", "v120", "v121", "3");
+        else TSG_FLAT_CALL("", "+{v[120:127]}", "v120", "v121", "3");
     }
-    flat_quad<NW, NEG>(work, xa, cc, acc);
-    flat_quad<NW, NEG>(work, xb, cc, acc);
 }
 
 // LDS-DMA of X^T chunk j (127 rows x 128 M) into buffer `buf`: 64 pieces of
@@ -582,8 +699,8 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
             uint32_t h8[8];
 #pragma unroll
             for (int i = 0; i < 8; i++) h8[i] = hw[i];
-            if (q < nch) walk_chunk_flat<NW, false>(accv, h8, ib, lanec, lds);  // +1 runs
-            else walk_chunk_flat<NW, true>(accv, h8, ib, lanec, lds);           // -1 runs
+            if (q < nch) walk_chunk_flat<NW, false>(accv, h8, ib, lanec);  // +1 runs
+            else walk_chunk_flat<NW, true>(accv, h8, ib, lanec);           // -1 runs
         } else {
             uint32_t cw[NW / 4];
 #pragma unroll

@@ -137,8 +137,10 @@ int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
                 }
                 if (flat) {
                     size_t D = img.ent.size() - sub0 - hdr_words;
-                    if (D & 1) {  // even: the kernel walks dword pairs; the extra dword of
-                        // +0.0f-row entries joins the last non-empty segment
+                    // D a multiple of 4: the kernel's pipeline walks index
+                    // batches of 4 dwords; the extra dwords of +0.0f-row
+                    // entries join the last non-empty segment
+                    while (D & 3) {
                         img.ent.push_back(0x01010101u * ((uint32_t)kSZeroRow | par));
                         const int c = last_nonempty;
                         img.ent[sub0 + 2 + c / kEntPerWord] += 1u << (8 * (c % kEntPerWord));
