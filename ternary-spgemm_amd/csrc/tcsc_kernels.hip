@@ -758,6 +758,146 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
     }
 }
 
+
+// ------------------------------------------------------------ rx kernel --
+// Register-X walk (see tsg_internal.h "rx"): the block's X rows live in
+// VGPRs and each entry is a SRC1-relative v_pk_add pair; no LDS read per
+// entry.  The block loop is generated inline asm (gen_rx_asm.py).
+#include "tsg_rx_asm.inc"
+
+typedef float F32x32 __attribute__((ext_vector_type(32)));
+
+template <bool NEG>
+__device__ __forceinline__ void rx_walk(F32x32 &a0, F32x32 &a1, F32x32 &a2, F32x32 &a3,
+                                        const uint32_t *base, uint32_t &off, uint32_t &hdr,
+                                        uint32_t xb)
+{
+    uint32_t t, nhdr, m0s;
+    if constexpr (NEG)
+        asm volatile(TSG_RX_WALK_NEG
+                     : "+{v[112:143]}"(a0), "+{v[144:175]}"(a1), "+{v[176:207]}"(a2),
+                       "+{v[208:239]}"(a3), [off] "+s"(off), [hdr] "+s"(hdr), [t] "=&s"(t),
+                       [nhdr] "=&s"(nhdr), [m0s] "=&s"(m0s)
+                     : [base] "s"(base), [xb] "v"(xb)
+                     : TSG_RX_CLOBBERS);
+    else
+        asm volatile(TSG_RX_WALK_POS
+                     : "+{v[112:143]}"(a0), "+{v[144:175]}"(a1), "+{v[176:207]}"(a2),
+                       "+{v[208:239]}"(a3), [off] "+s"(off), [hdr] "+s"(hdr), [t] "=&s"(t),
+                       [nhdr] "=&s"(nhdr), [m0s] "=&s"(m0s)
+                     : [base] "s"(base), [xb] "v"(xb)
+                     : TSG_RX_CLOBBERS);
+}
+
+// X^T chunk j (kRxChunk rows x 256 M) -> LDS buffer buf: one 1 KiB row per
+// wave-instruction, 8 per wave.
+__device__ __forceinline__ void rx_stage(const float *__restrict__ XT, int Mp, int m0, int j, int buf,
+                                         int wave, int lane)
+{
+#pragma unroll
+    for (int i = 0; i < kRxChunk / kRxWaves; i++) {
+        const int r = wave * (kRxChunk / kRxWaves) + i;
+        glds16(XT + (size_t)(j * kRxChunk + r) * Mp + m0 + 4 * lane, (uint32_t)(buf * 65536 + r * 1024));
+    }
+}
+
+template <bool PRELU, bool STAMP>
+__global__ __launch_bounds__(512, 1) void tsg_tcsc_rx_kernel(
+    const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wstart,
+    const uint32_t *__restrict__ ent, const float *__restrict__ b, const float *__restrict__ alpha,
+    float *__restrict__ Y, int M, int N, int nch, int mtiles, int ntiles,
+    unsigned long long *__restrict__ stamps)
+{
+    unsigned long long st_work = 0, st_wait = 0, st_t0 = 0;
+    if (STAMP) st_t0 = __builtin_amdgcn_s_memtime();
+    __shared__ __attribute__((aligned(16))) char lds[kRxLdsBytes];
+    const int tid = threadIdx.x, lane = tid & 63;
+    // LDS is only touched from asm (LDS-DMA, ds_read_b128 at absolute offsets
+    // from 0): a never-taken C++ store keeps the allocation in the kernel
+    if (M < 0) lds[tid] = 0;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // XCD-aware bijective remap, as in the stream kernel
+    const int T = mtiles * ntiles, L = blockIdx.x;
+    const int xcd = L & 7, slot = L >> 3, q8 = T >> 3, r8 = T & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+    // n-tile-major: the concurrent workgroups of an XCD share few column
+    // tiles, so their entry streams (latency-critical scalar loads) stay in
+    // that XCD's L2; X^T chunks arrive by LDS-DMA a whole step ahead.
+    const int nt = wg / mtiles, mt = wg - nt * mtiles;
+    const int m0 = mt * kRxTileM;
+    const int ncol0 = nt * kRxTileCols + wave * kRxNW;
+
+    // the walk addresses its stream as ent + off (bytes; SMEM base + SGPR offset)
+    uint32_t off = 4u * __builtin_amdgcn_readfirstlane(wstart[(size_t)nt * kRxWaves + wave]);
+    uint32_t hdr = __builtin_amdgcn_readfirstlane(ent[off / 4]);
+    rx_stage(XT, Mp, m0, 0, 0, wave, lane);
+    F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // two loops (not one with a branch per step: a uniform if/else between
+    // the two walks trips hipcc's SGPR-copy fixup on the asm operands)
+    const int steps = 2 * nch;
+    for (int q = 0; q < nch; q++) {  // +1 runs, ascending K
+        if (q + 1 < steps) rx_stage(XT, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
+        const unsigned long long ta = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        rx_walk<false>(a0, a1, a2, a3, ent, off, hdr, (uint32_t)(q & 1) * 65536u + (uint32_t)lane * 16u);
+        const unsigned long long tb = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (STAMP) {
+            const unsigned long long tc = __builtin_amdgcn_s_memtime();
+            st_work += tb - ta;
+            st_wait += tc - tb;
+        }
+    }
+    for (int q = nch; q < steps; q++) {  // -1 runs, ascending K
+        if (q + 1 < steps) rx_stage(XT, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
+        const unsigned long long ta = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        rx_walk<true>(a0, a1, a2, a3, ent, off, hdr, (uint32_t)(q & 1) * 65536u + (uint32_t)lane * 16u);
+        const unsigned long long tb = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (STAMP) {
+            const unsigned long long tc = __builtin_amdgcn_s_memtime();
+            st_work += tb - ta;
+            st_wait += tc - tb;
+        }
+    }
+    if (STAMP && lane == 0) {
+        unsigned long long *o = stamps + ((size_t)blockIdx.x * kRxWaves + wave) * 4;
+        o[0] = st_work;
+        o[1] = st_wait;
+        o[2] = __builtin_amdgcn_s_memtime() - st_t0;
+        o[3] = (unsigned long long)((nt << 16) | mt);
+    }
+    if (ncol0 >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int m = m0 + 4 * lane + r;
+        if (m >= M) continue;
+        float *yrow = Y + (size_t)m * N + ncol0;
+        float v[kRxNW];
+#pragma unroll
+        for (int c = 0; c < kRxNW; c++) {
+            const int n = ncol0 + c < N ? ncol0 + c : N - 1;
+            const float acc = c < 8 ? a0[4 * (c & 7) + r] : c < 16 ? a1[4 * (c & 7) + r]
+                             : c < 24 ? a2[4 * (c & 7) + r] : a3[4 * (c & 7) + r];
+            float y = acc + b[n];                       // comp.h:63
+            if (PRELU) y = (y > 0) ? y : alpha[n] * y;  // comp_prelu.h:57-67
+            v[c] = y;
+        }
+        if (ncol0 + kRxNW <= N && ((((size_t)m * N + ncol0) & 3) == 0)) {
+#pragma unroll
+            for (int c = 0; c < kRxNW; c += 4)
+                *reinterpret_cast<float4 *>(yrow + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
+        } else {
+#pragma unroll
+            for (int c = 0; c < kRxNW; c++)
+                if (ncol0 + c < N) yrow[c] = v[c];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launchers --
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream)
 {
@@ -829,6 +969,25 @@ int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const ui
     TSG_NW(4)
 #undef TSG_NW
     return -2;
+}
+
+int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
+                   const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
+                   int prelu, unsigned long long *stamps, void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    const int mtiles = Mp / kRxTileM, ntiles = Npad / kRxTileCols;
+    const dim3 grid((unsigned)(mtiles * ntiles)), block(kRxWaves * kLanes);
+    if (stamps)
+        hipLaunchKernelGGL((tsg_tcsc_rx_kernel<false, true>), grid, block, 0, s, XT, Mp, wstart, ent, b,
+                           alpha, Y, M, N, nch, mtiles, ntiles, stamps);
+    else if (prelu)
+        hipLaunchKernelGGL((tsg_tcsc_rx_kernel<true, false>), grid, block, 0, s, XT, Mp, wstart, ent, b,
+                           alpha, Y, M, N, nch, mtiles, ntiles, nullptr);
+    else
+        hipLaunchKernelGGL((tsg_tcsc_rx_kernel<false, false>), grid, block, 0, s, XT, Mp, wstart, ent, b,
+                           alpha, Y, M, N, nch, mtiles, ntiles, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace tsg

@@ -31,9 +31,13 @@ static int fail(int code, const std::string &msg)
 struct tsg_tcsc {
     int K = 0, N = 0, device = 0;
     int64_t nnz_pos = 0, nnz_neg = 0;
-    bool stream_kernel = true;            // TSG_KERNEL=chunked: v1 kernel; =flat: flat-stream variant
+    // kernel family: TSG_KERNEL=chunked (round-1 v1), pair / flat (LDS-gather
+    // stream kernel, two walks), rx (register-X kernel)
+    enum Kind { kChunked, kStream, kRx } kind = kStream;
+    bool stream_kernel = true;            // kind == kStream
     tsg::Image img;                       // v1 device image (chunked kernel)
     tsg::StreamImage simg;                // device image of the stream kernel
+    tsg::RxImage rimg;                    // device image of the rx kernel
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
@@ -81,8 +85,11 @@ int check_device(int dev)
 
 int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp)
 {
-    Mp = ((std::max(M, 1) + tsg::kTileM - 1) / tsg::kTileM) * tsg::kTileM;
-    Kp = h->stream_kernel ? h->simg.nch * tsg::kSChunk : h->img.nch * tsg::kChunkK;
+    const int tm = h->kind == tsg_tcsc::kRx ? tsg::kRxTileM : tsg::kTileM;
+    Mp = ((std::max(M, 1) + tm - 1) / tm) * tm;
+    Kp = h->kind == tsg_tcsc::kRx       ? h->rimg.nch * tsg::kRxChunk
+         : h->kind == tsg_tcsc::kStream ? h->simg.nch * tsg::kSChunk
+                                        : h->img.nch * tsg::kChunkK;
     return TSG_OK;
 }
 
@@ -161,11 +168,16 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     unsigned long long *stamps = nullptr;
     size_t nstamp = 0;
-    if (h->stream_kernel && std::getenv("TSG_STAMPS")) {  // diagnostic build path (never timed)
-        nstamp = (size_t)(Mp / tsg::kTileM) * (h->simg.Npad / h->simg.tile_cols) * tsg::kSWaves * 4;
+    if (h->kind != tsg_tcsc::kChunked && std::getenv("TSG_STAMPS")) {  // diagnostic path (never timed)
+        nstamp = h->kind == tsg_tcsc::kRx
+            ? (size_t)(Mp / tsg::kRxTileM) * (h->rimg.Npad / tsg::kRxTileCols) * tsg::kRxWaves * 4
+            : (size_t)(Mp / tsg::kTileM) * (h->simg.Npad / h->simg.tile_cols) * tsg::kSWaves * 4;
         HIP_TRY(hipMalloc(&stamps, nstamp * 8));
     }
-    const int lrc = h->stream_kernel
+    const int lrc = h->kind == tsg_tcsc::kRx
+        ? tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
+                              h->rimg.nch, prelu ? 1 : 0, stamps, s)
+        : h->stream_kernel
         ? tsg::launch_tcsc_stream(h->d_work, Mp, h->d_seg, h->d_ent, h->d_zero, db, dalpha, dY, M, N,
                                   h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, stamps,
                                   h->simg.flat, s)
@@ -189,7 +201,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         std::fprintf(stderr, "[tsg stamps] waves=%zu mean cycles/wave: total %.0f walk %.0f (%.1f%%) "
                              "barrier-wait %.0f (%.1f%%) max-walk %.0f steps=%d\n",
                      nw, tot / nw, work / nw, 100 * work / tot, wait / nw, 100 * wait / tot, wmax,
-                     2 * h->simg.nch);
+                     2 * (h->kind == tsg_tcsc::kRx ? h->rimg.nch : h->simg.nch));
     }
     if (slot >= 0) {
         HIP_TRY(hipEventRecord(h->ev1[slot], s));
@@ -295,9 +307,17 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     if (h->nnz_pos) h->rip.assign(rip, rip + h->nnz_pos);
     if (h->nnz_neg) h->rin.assign(rin, rin + h->nnz_neg);
     const char *kenv = std::getenv("TSG_KERNEL");
-    h->stream_kernel = !(kenv && std::strcmp(kenv, "chunked") == 0);
+    const bool want_rx = kenv && std::strcmp(kenv, "rx") == 0;
+    h->kind = want_rx ? tsg_tcsc::kRx
+              : (kenv && std::strcmp(kenv, "chunked") == 0) ? tsg_tcsc::kChunked
+                                                             : tsg_tcsc::kStream;
+    h->stream_kernel = h->kind == tsg_tcsc::kStream;
     const std::vector<uint32_t> *segv, *entv;
-    if (h->stream_kernel) {
+    if (h->kind == tsg_tcsc::kRx) {
+        tsg::build_rx_image(csp, csn, rip, rin, K, N, h->rimg);
+        segv = &h->rimg.wstart;
+        entv = &h->rimg.ent;
+    } else if (h->stream_kernel) {
         tsg::plan_stream_image(csp, csn, rip, rin, K, N, kenv && std::strcmp(kenv, "flat") == 0,
                                h->simg);
         segv = &h->simg.wstart;
@@ -412,12 +432,14 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     o->nnz_pos = h->nnz_pos;
     o->nnz_neg = h->nnz_neg;
     o->tcsc_bytes = 4 * (2 * ((int64_t)h->N + 1) + h->nnz_pos + h->nnz_neg);
-    o->image_bytes = h->stream_kernel ? (int64_t)(h->simg.wstart.size() + h->simg.ent.size()) * 4
-                                      : (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;
+    const bool rx = h->kind == tsg_tcsc::kRx;
+    o->image_bytes = rx ? (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4
+                     : h->stream_kernel ? (int64_t)(h->simg.wstart.size() + h->simg.ent.size()) * 4
+                                        : (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;
-    o->chunk_rows = h->stream_kernel ? tsg::kSChunk : tsg::kChunkK;
-    o->tile_rows = tsg::kTileM;
-    o->tile_cols = h->stream_kernel ? h->simg.tile_cols : h->img.tile_cols;
+    o->chunk_rows = rx ? tsg::kRxChunk : h->stream_kernel ? tsg::kSChunk : tsg::kChunkK;
+    o->tile_rows = rx ? tsg::kRxTileM : tsg::kTileM;
+    o->tile_cols = rx ? tsg::kRxTileCols : h->stream_kernel ? h->simg.tile_cols : h->img.tile_cols;
     return TSG_OK;
 }
 

@@ -2,6 +2,8 @@
 // the device-image planner, TCSC validation / column slicing for sharding,
 // and the synthetic-input generators used by bench.py and the driver.
 #include <algorithm>
+#include <climits>
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -168,6 +170,73 @@ void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
         if (build_stream_image(csp, csn, rip, rin, K, N, nw, flat, img) <= kSSubMax) return;
     }
     build_stream_image(csp, csn, rip, rin, K, N, 4, flat, img);  // 8 + 4*32+1 dwords always fit
+}
+
+void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                    const int32_t *rin, int K, int N, RxImage &img)
+{
+    img.K = K;
+    img.N = N;
+    img.Npad = ((N + kRxTileCols - 1) / kRxTileCols) * kRxTileCols;
+    img.nch = std::max(1, (K + kRxChunk - 1) / kRxChunk);
+    const int nch = img.nch, ntiles = img.Npad / kRxTileCols;
+    img.wstart.assign((size_t)ntiles * kRxWaves, 0u);
+    img.ent.clear();
+    const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
+    img.ent.reserve((size_t)(nnz / 48) * kRxBlockWords + (size_t)ntiles * kRxWaves * 2 * nch * kRxBlockWords);
+    std::vector<int32_t> cur((size_t)kRxNW * 2), end((size_t)kRxNW * 2);
+    for (int t = 0; t < ntiles; t++) {
+        for (int w = 0; w < kRxWaves; w++) {
+            const int n0 = t * kRxTileCols + w * kRxNW;
+            img.wstart[(size_t)t * kRxWaves + w] = (uint32_t)img.ent.size();
+            for (int c = 0; c < kRxNW; c++)
+                for (int p = 0; p < 2; p++) {
+                    const int n = n0 + c;
+                    const int32_t *cs = p ? csn : csp;
+                    cur[(size_t)c * 2 + p] = n < N ? cs[n] : 0;
+                    end[(size_t)c * 2 + p] = n < N ? cs[n + 1] : 0;
+                }
+            for (int q = 0; q < 2 * nch; q++) {
+                const int p = q / nch, j = q % nch;
+                const int32_t *ri = p ? rin : rip;
+                const int klo = j * kRxChunk, khi = klo + kRxChunk;
+                size_t last = SIZE_MAX;
+                for (;;) {
+                    int k0 = INT32_MAX;
+                    for (int c = 0; c < kRxNW; c++) {
+                        const int32_t i = cur[(size_t)c * 2 + p];
+                        if (i < end[(size_t)c * 2 + p] && ri[i] < khi) k0 = std::min(k0, (int)ri[i]);
+                    }
+                    if (k0 == INT32_MAX) break;
+                    // block rows [k0, kend): at most kRxBlockRows, inside the chunk,
+                    // at most kRxCap entries per column
+                    int kend = std::min(k0 + kRxBlockRows, khi);
+                    for (int c = 0; c < kRxNW; c++) {
+                        const int32_t i = cur[(size_t)c * 2 + p] + kRxCap;
+                        if (i < end[(size_t)c * 2 + p] && ri[i] < kend) kend = ri[i];
+                    }
+                    last = img.ent.size();
+                    img.ent.resize(last + kRxBlockWords, 0u);
+                    img.ent[last] = (uint32_t)(k0 - klo) * 1024u;
+                    for (int c = 0; c < kRxNW; c++) {
+                        int32_t &i = cur[(size_t)c * 2 + p];
+                        uint64_t bytes = 0;
+                        int f = 0;
+                        for (; i < end[(size_t)c * 2 + p] && ri[i] < kend; i++, f++)
+                            bytes |= (uint64_t)(4u * (uint32_t)(ri[i] - k0 + 1)) << (8 * f);
+                        img.ent[last + 2 + 2 * c] = (uint32_t)bytes;
+                        img.ent[last + 3 + 2 * c] = (uint32_t)(bytes >> 32);
+                    }
+                }
+                if (last == SIZE_MAX) {  // no entries in this step: one empty block
+                    last = img.ent.size();
+                    img.ent.resize(last + kRxBlockWords, 0u);
+                }
+                img.ent[last] |= 1u << 31;
+            }
+        }
+    }
+    img.ent.resize(img.ent.size() + kRxBlockWords, 0u);  // the walk reads one header ahead
 }
 
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,

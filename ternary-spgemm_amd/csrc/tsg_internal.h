@@ -63,6 +63,40 @@ void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
                        const int32_t *rin, int K, int N, bool flat, StreamImage &img);
 
 // ---------------------------------------------------------------------------
+// "rx" (register-X) kernel (tsg_tcsc_rx_kernel)
+//
+// Workgroup: 256 M rows (4 per lane) x 8 waves x 32 columns, 512 threads,
+// 256 VGPRs per wave.  X^T chunks of kRxChunk rows are staged in LDS (1 KiB
+// per row, double buffered); a wave walks its columns in BLOCKS of at most
+// kRxBlockRows consecutive K rows: the block's X rows are loaded into VGPRs
+// (ds_read_b128) and every entry is one s_set_gpr_idx_idx (SRC1-relative
+// X slot) + two v_pk_add_f32 -- no LDS traffic per entry.  A block holds at
+// most kRxCap entries per column (the builder cuts blocks so it does).
+constexpr int kRxTileM = 256;
+constexpr int kRxWaves = 8;
+constexpr int kRxNW = 32;
+constexpr int kRxTileCols = kRxWaves * kRxNW;  // 256
+constexpr int kRxChunk = 64;                   // K rows per LDS chunk
+constexpr int kRxBlockRows = 24;
+constexpr int kRxCap = 8;
+constexpr int kRxBlockWords = 2 + 2 * kRxNW;  // [hdr][0][column c: 2 dwords of entry bytes]
+constexpr int kRxLdsBytes = 2 * 65536 + kRxBlockRows * 1024;  // 2 chunks + over-read pad
+
+// Stream of one wave: for every step q = p*nch + j (p = 0: +1 entries, p = 1:
+// -1 entries; chunk j) one or more blocks of kRxBlockWords dwords:
+//   hdr = (k0 - j*kRxChunk) * 1024 | (last block of the step) << 31
+//   column c: 8 bytes, entry byte 4*(k - k0 + 1) for its entries of the
+//   block, ascending k, then 0 bytes (0 = "empty": the kernel adds X slot 0,
+//   which is +0.0f).
+struct RxImage {
+    int K = 0, N = 0, Npad = 0, nch = 0;
+    std::vector<uint32_t> wstart;   // per (column tile, wave): first dword of its stream
+    std::vector<uint32_t> ent;
+};
+void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                    const int32_t *rin, int K, int N, RxImage &img);
+
+// ---------------------------------------------------------------------------
 // "chunked" kernel (tsg_tcsc_lds_kernel, round-1 v1, kept for A/B)
 constexpr int kChunkK = 128;        // K rows of X^T staged in LDS per chunk
 constexpr int kZeroRow = kChunkK;   // LDS row holding +0.0f (pads index groups)
@@ -90,5 +124,8 @@ int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const ui
                        const float *zero, const float *b, const float *alpha, float *Y, int M,
                        int N, int Npad, int nch, int nw, int prelu, unsigned long long *stamps,
                        bool flat, void *stream);
+int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
+                   const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
+                   int prelu, unsigned long long *stamps, void *stream);
 
 }  // namespace tsg
