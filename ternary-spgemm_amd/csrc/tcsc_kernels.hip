@@ -763,7 +763,13 @@ __global__ __launch_bounds__(1024, 1) void tsg_tcsc_stream_kernel(
 // Register-X walk (see tsg_internal.h "rx"): the block's X rows live in
 // VGPRs and each entry is a SRC1-relative v_pk_add pair; no LDS read per
 // entry.  The block loop is generated inline asm (gen_rx_asm.py).
+#ifdef TSG_RX_INC
+#include TSG_RX_INC  // diagnostic variant of the generated walk
+#else
 #include "tsg_rx_asm.inc"
+#endif
+#define TSG_RX_CAT2(a, b) a##b
+#define TSG_RX_CAT(a, b) TSG_RX_CAT2(a, b)
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 
@@ -774,19 +780,19 @@ __device__ __forceinline__ void rx_walk(F32x32 &a0, F32x32 &a1, F32x32 &a2, F32x
 {
     uint32_t t, nhdr, m0s;
     if constexpr (NEG)
-        asm volatile(TSG_RX_WALK_NEG
+        asm volatile(TSG_RX_CAT(TSG_RX_WALK_NEG_R, TSG_RX_ROWS)
                      : "+{v[112:143]}"(a0), "+{v[144:175]}"(a1), "+{v[176:207]}"(a2),
                        "+{v[208:239]}"(a3), [off] "+s"(off), [hdr] "+s"(hdr), [t] "=&s"(t),
                        [nhdr] "=&s"(nhdr), [m0s] "=&s"(m0s)
                      : [base] "s"(base), [xb] "v"(xb)
-                     : TSG_RX_CLOBBERS);
+                     : TSG_RX_CAT(TSG_RX_CLOBBERS_R, TSG_RX_ROWS));
     else
-        asm volatile(TSG_RX_WALK_POS
+        asm volatile(TSG_RX_CAT(TSG_RX_WALK_POS_R, TSG_RX_ROWS)
                      : "+{v[112:143]}"(a0), "+{v[144:175]}"(a1), "+{v[176:207]}"(a2),
                        "+{v[208:239]}"(a3), [off] "+s"(off), [hdr] "+s"(hdr), [t] "=&s"(t),
                        [nhdr] "=&s"(nhdr), [m0s] "=&s"(m0s)
                      : [base] "s"(base), [xb] "v"(xb)
-                     : TSG_RX_CLOBBERS);
+                     : TSG_RX_CAT(TSG_RX_CLOBBERS_R, TSG_RX_ROWS));
 }
 
 // X^T chunk j (kRxChunk rows x 256 M) -> LDS buffer buf: one 1 KiB row per
@@ -797,12 +803,20 @@ __device__ __forceinline__ void rx_stage(const float *__restrict__ XT, int Mp, i
 #pragma unroll
     for (int i = 0; i < kRxChunk / kRxWaves; i++) {
         const int r = wave * (kRxChunk / kRxWaves) + i;
-        glds16(XT + (size_t)(j * kRxChunk + r) * Mp + m0 + 4 * lane, (uint32_t)(buf * 65536 + r * 1024));
+        glds16(XT + (size_t)(j * kRxChunk + r) * Mp + m0 + 4 * lane, (uint32_t)(buf * kRxChunkBytes + r * 1024));
     }
 }
 
+// TSG_RX_DIAG_NOSYNC: diagnostic build only -- no chunk staging and no step
+// barriers (results are WRONG; times the bare block walk).
+#ifdef TSG_RX_DIAG_NOSYNC
+constexpr bool kRxDiagNoSync = true;
+#else
+constexpr bool kRxDiagNoSync = false;
+#endif
+
 template <bool PRELU, bool STAMP>
-__global__ __launch_bounds__(512, 1) void tsg_tcsc_rx_kernel(
+__global__ __launch_bounds__(kRxWaves * 64, 8 / kRxWaves) void tsg_tcsc_rx_kernel(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wstart,
     const uint32_t *__restrict__ ent, const float *__restrict__ b, const float *__restrict__ alpha,
     float *__restrict__ Y, int M, int N, int nch, int mtiles, int ntiles,
@@ -838,12 +852,14 @@ __global__ __launch_bounds__(512, 1) void tsg_tcsc_rx_kernel(
     // the two walks trips hipcc's SGPR-copy fixup on the asm operands)
     const int steps = 2 * nch;
     for (int q = 0; q < nch; q++) {  // +1 runs, ascending K
-        if (q + 1 < steps) rx_stage(XT, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
+        if (!kRxDiagNoSync && q + 1 < steps) rx_stage(XT, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
         const unsigned long long ta = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-        rx_walk<false>(a0, a1, a2, a3, ent, off, hdr, (uint32_t)(q & 1) * 65536u + (uint32_t)lane * 16u);
+        rx_walk<false>(a0, a1, a2, a3, ent, off, hdr, (uint32_t)(q & 1) * (uint32_t)kRxChunkBytes + (uint32_t)lane * 16u);
         const unsigned long long tb = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (!kRxDiagNoSync) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         if (STAMP) {
             const unsigned long long tc = __builtin_amdgcn_s_memtime();
             st_work += tb - ta;
@@ -851,12 +867,14 @@ __global__ __launch_bounds__(512, 1) void tsg_tcsc_rx_kernel(
         }
     }
     for (int q = nch; q < steps; q++) {  // -1 runs, ascending K
-        if (q + 1 < steps) rx_stage(XT, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
+        if (!kRxDiagNoSync && q + 1 < steps) rx_stage(XT, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
         const unsigned long long ta = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-        rx_walk<true>(a0, a1, a2, a3, ent, off, hdr, (uint32_t)(q & 1) * 65536u + (uint32_t)lane * 16u);
+        rx_walk<true>(a0, a1, a2, a3, ent, off, hdr, (uint32_t)(q & 1) * (uint32_t)kRxChunkBytes + (uint32_t)lane * 16u);
         const unsigned long long tb = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (!kRxDiagNoSync) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         if (STAMP) {
             const unsigned long long tc = __builtin_amdgcn_s_memtime();
             st_work += tb - ta;

@@ -72,15 +72,31 @@ void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
 // (ds_read_b128) and every entry is one s_set_gpr_idx_idx (SRC1-relative
 // X slot) + two v_pk_add_f32 -- no LDS traffic per entry.  A block holds at
 // most kRxCap entries per column (the builder cuts blocks so it does).
+// Variant knobs (compile-time, -DTSG_RX_*): waves per workgroup (4: two
+// workgroups share a CU so one's barrier/latency stalls are covered by the
+// other; 8: one per CU), K rows per LDS chunk, K rows per register block.
+#ifndef TSG_RX_WAVES
+#define TSG_RX_WAVES 4
+#endif
+#ifndef TSG_RX_CHUNK
+#define TSG_RX_CHUNK 32
+#endif
+#ifndef TSG_RX_ROWS
+#define TSG_RX_ROWS 16
+#endif
 constexpr int kRxTileM = 256;
-constexpr int kRxWaves = 8;
+constexpr int kRxWaves = TSG_RX_WAVES;
 constexpr int kRxNW = 32;
-constexpr int kRxTileCols = kRxWaves * kRxNW;  // 256
-constexpr int kRxChunk = 64;                   // K rows per LDS chunk
-constexpr int kRxBlockRows = 24;
+constexpr int kRxTileCols = kRxWaves * kRxNW;
+constexpr int kRxChunk = TSG_RX_CHUNK;         // K rows per LDS chunk
+constexpr int kRxChunkBytes = kRxChunk * 1024;
+constexpr int kRxBlockRows = TSG_RX_ROWS;
 constexpr int kRxCap = 8;
 constexpr int kRxBlockWords = 2 + 2 * kRxNW;  // [hdr][0][column c: 2 dwords of entry bytes]
-constexpr int kRxLdsBytes = 2 * 65536 + kRxBlockRows * 1024;  // 2 chunks + over-read pad
+// 2 chunks + the over-read of a block that starts on a chunk's last row
+constexpr int kRxLdsBytes = 2 * kRxChunkBytes + (kRxBlockRows - 1) * 1024;
+static_assert(kRxChunk % kRxWaves == 0, "chunk rows split over waves");
+static_assert(kRxLdsBytes * (8 / kRxWaves) <= 160 * 1024, "workgroups per CU must fit the 160 KiB LDS");
 
 // Stream of one wave: for every step q = p*nch + j (p = 0: +1 entries, p = 1:
 // -1 entries; chunk j) one or more blocks of kRxBlockWords dwords:
