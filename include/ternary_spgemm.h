@@ -150,6 +150,16 @@ int tsg_csc_packed_to_tcsc(const int32_t *col_ptr, const int32_t *row_idx, const
                            int32_t *row_index_pos, int32_t *row_index_neg, int64_t *nnz_pos,
                            int64_t *nnz_neg);
 
+/* Machine code of the weight-compiled kernel (TSG_KERNEL=jit) for a TCSC:
+ * the generated gfx950 region (uint32 words; region byte offset 0 = word 0)
+ * and, per (256-column tile, wave), the byte offset of that wave's stream.
+ * Host only (no GPU): lets tests decode and emulate the code the device will
+ * run.  NULL buffers query the lengths (in elements). */
+int tsg_jit_codegen(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                    const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                    uint32_t *code, int64_t code_cap, int64_t *code_len,
+                    uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+
 /* X[i] = integer-valued fp32 U{-range..range} (initX, sparseUtils.h:6-23). */
 int tsg_gen_x(int64_t len, int range, uint64_t seed, float *X);
 

@@ -32,12 +32,17 @@ struct tsg_tcsc {
     int K = 0, N = 0, device = 0;
     int64_t nnz_pos = 0, nnz_neg = 0;
     // kernel family: TSG_KERNEL=chunked (round-1 v1), pair / flat (LDS-gather
-    // stream kernel, two walks), rx (register-X kernel)
-    enum Kind { kChunked, kStream, kRx } kind = kStream;
+    // stream kernel, two walks), rx (register-X kernel), jit (weight-compiled)
+    enum Kind { kChunked, kStream, kRx, kJit } kind = kStream;
     bool stream_kernel = true;            // kind == kStream
     tsg::Image img;                       // v1 device image (chunked kernel)
     tsg::StreamImage simg;                // device image of the stream kernel
     tsg::RxImage rimg;                    // device image of the rx kernel
+    tsg::JitImage jimg;                   // generated code of the jit kernel (code freed once loaded)
+    tsg::JitModule jmod;                  // dispatcher + generated code, loaded
+    uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
+    bool jit_checked = false;             // status read back once after the first launch
+    int64_t jit_code_bytes = 0;
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
@@ -85,9 +90,10 @@ int check_device(int dev)
 
 int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp)
 {
-    const int tm = h->kind == tsg_tcsc::kRx ? tsg::kRxTileM : tsg::kTileM;
+    const int tm = h->kind == tsg_tcsc::kRx ? tsg::kRxTileM : h->kind == tsg_tcsc::kJit ? tsg::kJitTileM : tsg::kTileM;
     Mp = ((std::max(M, 1) + tm - 1) / tm) * tm;
-    Kp = h->kind == tsg_tcsc::kRx       ? h->rimg.nch * tsg::kRxChunk
+    Kp = h->kind == tsg_tcsc::kJit      ? h->jimg.nch * tsg::kJitChunk
+         : h->kind == tsg_tcsc::kRx     ? h->rimg.nch * tsg::kRxChunk
          : h->kind == tsg_tcsc::kStream ? h->simg.nch * tsg::kSChunk
                                         : h->img.nch * tsg::kChunkK;
     return TSG_OK;
@@ -168,13 +174,16 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     unsigned long long *stamps = nullptr;
     size_t nstamp = 0;
-    if (h->kind != tsg_tcsc::kChunked && std::getenv("TSG_STAMPS")) {  // diagnostic path (never timed)
+    if (h->kind != tsg_tcsc::kChunked && h->kind != tsg_tcsc::kJit && std::getenv("TSG_STAMPS")) {  // diagnostic path (never timed)
         nstamp = h->kind == tsg_tcsc::kRx
             ? (size_t)(Mp / tsg::kRxTileM) * (h->rimg.Npad / tsg::kRxTileCols) * tsg::kRxWaves * 4
             : (size_t)(Mp / tsg::kTileM) * (h->simg.Npad / h->simg.tile_cols) * tsg::kSWaves * 4;
         HIP_TRY(hipMalloc(&stamps, nstamp * 8));
     }
-    const int lrc = h->kind == tsg_tcsc::kRx
+    const int lrc = h->kind == tsg_tcsc::kJit
+        ? tsg::launch_tcsc_jit(h->jmod, h->d_work, Mp, h->d_seg, db, dalpha, dY, M, N, h->jimg.Npad,
+                               h->jimg.nch, prelu ? 1 : 0, h->d_status, s)
+        : h->kind == tsg_tcsc::kRx
         ? tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, stamps, s)
         : h->stream_kernel
@@ -202,6 +211,14 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
                              "barrier-wait %.0f (%.1f%%) max-walk %.0f steps=%d\n",
                      nw, tot / nw, work / nw, 100 * work / tot, wait / nw, 100 * wait / tot, wmax,
                      2 * (h->kind == tsg_tcsc::kRx ? h->rimg.nch : h->simg.nch));
+    }
+    if (h->kind == tsg_tcsc::kJit && !h->jit_checked) {
+        // one-time check that the dispatcher found the generated region
+        uint32_t st = 0;
+        HIP_TRY(hipMemcpyAsync(&st, h->d_status, sizeof st, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (st != 0) return fail(TSG_ERR_HIP, "jit kernel: generated code region not found (status " + std::to_string(st) + ")");
+        h->jit_checked = true;
     }
     if (slot >= 0) {
         HIP_TRY(hipEventRecord(h->ev1[slot], s));
@@ -253,8 +270,9 @@ void free_handle(tsg_tcsc *h)
     DeviceGuard g(h->device);
     if (h->ring_count) (void)hipDeviceSynchronize();
     for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_zero, (void *)h->d_x,
-                    (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha})
+                    (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha, (void *)h->d_status})
         if (p) (void)hipFree(p);
+    h->jmod.unload();
     if (h->stream) (void)hipStreamDestroy(h->stream);
     for (int i = 0; i < tsg_tcsc::kRing; i++) {
         if (h->ev0[i]) (void)hipEventDestroy(h->ev0[i]);
@@ -308,12 +326,27 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     if (h->nnz_neg) h->rin.assign(rin, rin + h->nnz_neg);
     const char *kenv = std::getenv("TSG_KERNEL");
     const bool want_rx = kenv && std::strcmp(kenv, "rx") == 0;
-    h->kind = want_rx ? tsg_tcsc::kRx
+    const bool want_jit = kenv && std::strcmp(kenv, "jit") == 0;
+    h->kind = want_jit ? tsg_tcsc::kJit
+              : want_rx ? tsg_tcsc::kRx
               : (kenv && std::strcmp(kenv, "chunked") == 0) ? tsg_tcsc::kChunked
                                                              : tsg_tcsc::kStream;
     h->stream_kernel = h->kind == tsg_tcsc::kStream;
     const std::vector<uint32_t> *segv, *entv;
-    if (h->kind == tsg_tcsc::kRx) {
+    static const std::vector<uint32_t> kNoEntries(1, 0u);
+    if (h->kind == tsg_tcsc::kJit) {
+        tsg::build_jit_code(csp, csn, rip, rin, K, N, h->jimg);
+        h->jit_code_bytes = (int64_t)h->jimg.code.size() * 4;
+        DeviceGuard g0(device);
+        const std::string err = h->jmod.load(h->jimg.code);
+        std::vector<uint32_t>().swap(h->jimg.code);  // the loader holds its own copy
+        if (!err.empty()) {
+            free_handle(h);
+            return fail(TSG_ERR_HIP, "jit kernel: " + err);
+        }
+        segv = &h->jimg.wcode;
+        entv = &kNoEntries;
+    } else if (h->kind == tsg_tcsc::kRx) {
         tsg::build_rx_image(csp, csn, rip, rin, K, N, h->rimg);
         segv = &h->rimg.wstart;
         entv = &h->rimg.ent;
@@ -333,11 +366,11 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     if (hipMalloc(&h->d_seg, sb) != hipSuccess || hipMalloc(&h->d_ent, eb) != hipSuccess ||
         hipMalloc(&h->d_b, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
         hipMalloc(&h->d_alpha, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
-        hipMalloc(&h->d_zero, 256) != hipSuccess) {
+        hipMalloc(&h->d_zero, 256) != hipSuccess || hipMalloc(&h->d_status, 16) != hipSuccess) {
         free_handle(h);
         return fail(TSG_ERR_NOMEM, "hipMalloc of the device image failed");
     }
-    if (hipMemset(h->d_zero, 0, 256) != hipSuccess ||
+    if (hipMemset(h->d_zero, 0, 256) != hipSuccess || hipMemset(h->d_status, 0, 16) != hipSuccess ||
         hipMemcpy(h->d_seg, segv->data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->d_ent, entv->data(), eb, hipMemcpyHostToDevice) != hipSuccess) {
         free_handle(h);
@@ -432,14 +465,16 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     o->nnz_pos = h->nnz_pos;
     o->nnz_neg = h->nnz_neg;
     o->tcsc_bytes = 4 * (2 * ((int64_t)h->N + 1) + h->nnz_pos + h->nnz_neg);
-    const bool rx = h->kind == tsg_tcsc::kRx;
-    o->image_bytes = rx ? (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4
+    const bool rx = h->kind == tsg_tcsc::kRx || h->kind == tsg_tcsc::kJit;
+    o->image_bytes = h->kind == tsg_tcsc::kJit ? h->jit_code_bytes + (int64_t)h->jimg.wcode.size() * 4
+                     : rx ? (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4
                      : h->stream_kernel ? (int64_t)(h->simg.wstart.size() + h->simg.ent.size()) * 4
                                         : (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;
-    o->chunk_rows = rx ? tsg::kRxChunk : h->stream_kernel ? tsg::kSChunk : tsg::kChunkK;
-    o->tile_rows = rx ? tsg::kRxTileM : tsg::kTileM;
-    o->tile_cols = rx ? tsg::kRxTileCols : h->stream_kernel ? h->simg.tile_cols : h->img.tile_cols;
+    const bool jit = h->kind == tsg_tcsc::kJit;
+    o->chunk_rows = jit ? tsg::kJitChunk : rx ? tsg::kRxChunk : h->stream_kernel ? tsg::kSChunk : tsg::kChunkK;
+    o->tile_rows = jit ? tsg::kJitTileM : rx ? tsg::kRxTileM : tsg::kTileM;
+    o->tile_cols = jit ? tsg::kJitTileCols : rx ? tsg::kRxTileCols : h->stream_kernel ? h->simg.tile_cols : h->img.tile_cols;
     return TSG_OK;
 }
 

@@ -76,13 +76,13 @@ void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *ri
 // workgroups share a CU so one's barrier/latency stalls are covered by the
 // other; 8: one per CU), K rows per LDS chunk, K rows per register block.
 #ifndef TSG_RX_WAVES
-#define TSG_RX_WAVES 4
+#define TSG_RX_WAVES 8
 #endif
 #ifndef TSG_RX_CHUNK
-#define TSG_RX_CHUNK 32
+#define TSG_RX_CHUNK 64
 #endif
 #ifndef TSG_RX_ROWS
-#define TSG_RX_ROWS 16
+#define TSG_RX_ROWS 24
 #endif
 constexpr int kRxTileM = 256;
 constexpr int kRxWaves = TSG_RX_WAVES;
@@ -111,6 +111,37 @@ struct RxImage {
 };
 void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                     const int32_t *rin, int K, int N, RxImage &img);
+
+// ---------------------------------------------------------------------------
+// "jit" (weight-compiled) kernel: dispatcher tsg_jit_kernel (tsg_jit_kernel.hip,
+// built as the code object lib/tsg_jit.co) + machine code generated from the
+// TCSC arrays (tsg_jit.cpp).  Tiling as the rx kernel: 256 M rows x 8 waves x
+// 32 columns per workgroup, X^T chunks of 64 K rows double buffered in LDS.
+constexpr int kJitTileM = 256;
+constexpr int kJitWaves = 8;
+constexpr int kJitNW = 32;
+constexpr int kJitTileCols = kJitWaves * kJitNW;
+constexpr int kJitChunk = 64;
+constexpr int kJitSlots = 24;   // X slot registers v[8:103]
+constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
+
+struct JitImage {
+    int K = 0, N = 0, Npad = 0, nch = 0;
+    std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
+    std::vector<uint32_t> wcode;   // per (column tile, wave): byte offset of its stream
+};
+void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                    const int32_t *rin, int K, int N, JitImage &img);
+
+struct JitModule {
+    void *module = nullptr;        // hipModule_t
+    void *function = nullptr;      // hipFunction_t of tsg_jit_kernel
+    std::string load(const std::vector<uint32_t> &code);  // "" on success
+    void unload();
+};
+int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
+                    const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
+                    int prelu, uint32_t *status, void *stream);
 
 // ---------------------------------------------------------------------------
 // "chunked" kernel (tsg_tcsc_lds_kernel, round-1 v1, kept for A/B)

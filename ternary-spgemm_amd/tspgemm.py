@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_info", "tcsc_hip_to_dense", "tcsc_hip_set_timing", "tcsc_hip_kernel_time",
     "tcsc_hip_last_error", "tcsc_hip_device_count", "tsg_tcsc_slice", "tsg_tcsc_validate",
     "tsg_gen_tcsc", "tsg_gen_x", "tcsc_hip_create_csc_packed", "tsg_tcsc_to_csc_packed",
-    "tsg_csc_packed_to_tcsc",
+    "tsg_csc_packed_to_tcsc", "tsg_jit_codegen",
 )
 
 
@@ -106,6 +106,8 @@ def lib() -> C.CDLL:
     L.tsg_tcsc_to_csc_packed.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, vp, C.POINTER(C.c_int64)]
     L.tsg_csc_packed_to_tcsc.argtypes = [vp, vp, vp, C.c_int, vp, vp, vp, vp,
                                          C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.tsg_jit_codegen.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
+                                  C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     for f in EXPORTED_SYMBOLS:
         if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error"):
             getattr(L, f).restype = C.c_int
@@ -199,6 +201,22 @@ def csc_packed_to_tcsc(col_ptr, row_idx, packed, N: int):
                                     *(a.ctypes.data for a in o), C.byref(p), C.byref(q)),
            "tsg_csc_packed_to_tcsc")
     return o[0], o[1], o[2][: p.value], o[3][: q.value]
+
+
+def jit_codegen(csp, csn, rip, rin, K: int, N: int):
+    """Host-side machine code of the weight-compiled kernel (TSG_KERNEL=jit):
+    (region words uint32[], per-(tile, wave) stream byte offsets uint32[])."""
+    csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
+    nc, nw = C.c_int64(), C.c_int64()
+    L = lib()
+    _check(L.tsg_jit_codegen(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, None, 0,
+                             C.byref(nc), None, 0, C.byref(nw)), "tsg_jit_codegen")
+    code = np.empty(nc.value, np.uint32)
+    wcode = np.empty(nw.value, np.uint32)
+    _check(L.tsg_jit_codegen(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, _ptr(code),
+                             nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
+           "tsg_jit_codegen")
+    return code, wcode
 
 
 def gen_x(M: int, K: int, seed: int, rng: int = 512) -> np.ndarray:
