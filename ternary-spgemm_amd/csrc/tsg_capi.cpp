@@ -344,6 +344,10 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
             free_handle(h);
             return fail(TSG_ERR_HIP, "jit kernel: " + err);
         }
+        if (const char *d = std::getenv("TSG_JIT_DIAG"))  // diagnostic: every tile runs tile 0's code
+            if (std::strcmp(d, "samecode") == 0)
+                for (size_t i = tsg::kJitWaves; i < h->jimg.wcode.size(); i++)
+                    h->jimg.wcode[i] = h->jimg.wcode[i % tsg::kJitWaves];
         segv = &h->jimg.wcode;
         entv = &kNoEntries;
     } else if (h->kind == tsg_tcsc::kRx) {

@@ -115,14 +115,14 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 // ---------------------------------------------------------------------------
 // "jit" (weight-compiled) kernel: dispatcher tsg_jit_kernel (tsg_jit_kernel.hip,
 // built as the code object lib/tsg_jit.co) + machine code generated from the
-// TCSC arrays (tsg_jit.cpp).  Tiling as the rx kernel: 256 M rows x 8 waves x
-// 32 columns per workgroup, X^T chunks of 64 K rows double buffered in LDS.
-constexpr int kJitTileM = 256;
+// TCSC arrays (tsg_jit.cpp).  Workgroup: 128 M rows (2 per lane) x 8 waves x
+// 64 columns; X^T chunks of 96 K rows in a ring of 3 LDS buffers (144 KiB).
+constexpr int kJitTileM = 128;
 constexpr int kJitWaves = 8;
-constexpr int kJitNW = 32;
+constexpr int kJitNW = 64;
 constexpr int kJitTileCols = kJitWaves * kJitNW;
-constexpr int kJitChunk = 64;
-constexpr int kJitSlots = 24;   // X slot registers v[8:103]
+constexpr int kJitChunk = 96;
+constexpr int kJitSlots = 48;   // X slot registers v[8:103], 2 per slot
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
 
 struct JitImage {

@@ -28,31 +28,86 @@ namespace tsg {
 namespace {
 
 // --- gfx950 encodings (checked against llvm-mc -mcpu=gfx950 -show-encoding) ---
-// v_pk_add_f32 v[d:d+1], v[d:d+1], v[x:x+1] [neg_lo:[0,1] neg_hi:[0,1]]  (VOP3P)
-inline void emit_pk_add(std::vector<uint32_t> &c, uint32_t d, uint32_t x, bool neg)
-{
-    c.push_back(0xd3b24000u | d | (neg ? 0x200u : 0u));
-    c.push_back((3u << 27) | ((256u + x) << 9) | (256u + d) | (neg ? (2u << 29) : 0u));
-}
-// ds_read_b128 v[d:d+3], v[a] offset:off  (DS)
-inline void emit_ds_read_b128(std::vector<uint32_t> &c, uint32_t d, uint32_t a, uint32_t off)
-{
-    c.push_back(0xd9fe0000u | off);
-    c.push_back((d << 24) | a);
-}
-inline void emit_wait_lgkm0(std::vector<uint32_t> &c) { c.push_back(0xbf8cc07fu); }
-inline void emit_nop(std::vector<uint32_t> &c) { c.push_back(0xbf800000u); }
-// s_getpc_b64 s[92:93]; s_setpc_b64 s[94:95]
-inline void emit_return(std::vector<uint32_t> &c)
-{
-    c.push_back(0xbedc1c00u);
-    c.push_back(0xbe801d5eu);
-}
+struct Emit {
+    std::vector<uint32_t> &c;
+    // keep 8-byte instructions 8-byte aligned (hand-asm placement rule)
+    void align8()
+    {
+        if (c.size() & 1) c.push_back(0xbf800000u);  // s_nop 0
+    }
+    // v_pk_add_f32 v[d:d+1], v[d:d+1], v[x:x+1] [neg_lo:[0,1] neg_hi:[0,1]]  (VOP3P;
+    // the two halves are rows 0 and 1 of the lane: two IEEE adds)
+    void pk_add(uint32_t d, uint32_t x, bool neg)
+    {
+        align8();
+        c.push_back(0xd3b24000u | d | (neg ? 0x200u : 0u));
+        c.push_back((3u << 27) | ((256u + x) << 9) | (256u + d) | (neg ? (2u << 29) : 0u));
+    }
+    // ds_read_b64 v[d:d+1], v[a] offset:off
+    void ds_read_b64(uint32_t d, uint32_t a, uint32_t off)
+    {
+        align8();
+        c.push_back(0xd8ec0000u | off);
+        c.push_back((d << 24) | a);
+    }
+    // global_load_lds_dwordx4 v[voff], s[84:85]   (LDS-DMA, destination M0)
+    void glds_x4(uint32_t voff)
+    {
+        align8();
+        c.push_back(0xddf48000u);
+        c.push_back((84u << 16) | voff);
+    }
+    // global_load_dword v107, v114, s[88:89]   (code prefetch into L2)
+    void code_touch()
+    {
+        align8();
+        c.push_back(0xdc508000u);
+        c.push_back((107u << 24) | (88u << 16) | 114u);
+    }
+    void m0_lit(uint32_t v) { align8(); c.push_back(0xbefc00ffu); c.push_back(v); }  // s_mov_b32 m0, v
+    void save_m0() { c.push_back(0xbed6007cu); }      // s_mov_b32 s86, m0
+    void restore_m0() { c.push_back(0xbefc0056u); }   // s_mov_b32 m0, s86
+    void base_reset() { c.push_back(0xbed40150u); }   // s_mov_b64 s[84:85], s[80:81]
+    void base_next()                                  // s[84:85] += s82
+    {
+        c.push_back(0x80545254u);
+        c.push_back(0x82558055u);
+    }
+    void touch_addr(uint32_t region_off)              // s[88:89] = s[92:93] + off
+    {
+        align8();
+        c.push_back(0x8058ff5cu);
+        c.push_back(region_off);
+        c.push_back(0x8259805du);
+    }
+    void nop(uint32_t n = 0) { c.push_back(0xbf800000u | n); }
+    void wait_lgkm0() { c.push_back(0xbf8cc07fu); }
+    void wait_vm0() { c.push_back(0xbf8c0f70u); }
+    void barrier() { c.push_back(0xbf8a0000u); }
+    void ret() { c.push_back(0xbe801d5eu); }         // s_setpc_b64 s[94:95]
+    uint32_t pos_bytes() const { return (uint32_t)(c.size() * 4); }
+};
 
-constexpr uint32_t kXSlot0 = 8;     // v[8 + 4s : 11 + 4s], s < kJitSlots
-constexpr uint32_t kLdsBase0 = 104, kLdsBase1 = 105;
-constexpr uint32_t kAcc0 = 112;     // column c: v[112 + 4c : 115 + 4c]
+constexpr uint32_t kXSlot0 = 8;          // v[8 + 2s : 9 + 2s], s < kJitSlots
+constexpr uint32_t kLdsBaseV = 104;      // v104 + b: lane row 0 of LDS buffer b
+constexpr uint32_t kDmaOffV = 108;       // v108 + i: DMA piece i offsets
+constexpr uint32_t kAcc0 = 116;          // column c: v[116 + 2c : 117 + 2c]
 constexpr int kBlockRows = kJitSlots / 2;  // double-buffered X row blocks
+constexpr uint32_t kRowBytes = kJitTileM * 4;             // one X^T row of the tile in LDS
+constexpr uint32_t kBufBytes = kJitChunk * kRowBytes;     // one LDS chunk buffer
+constexpr int kPieces = kJitChunk / kJitWaves / 2;        // DMA pieces per wave per chunk
+constexpr uint32_t kTouchAhead = 8192;   // code prefetch window [pos + 8 KiB, pos + 24 KiB)
+constexpr int kTailPad = 8192 + 1024;    // words of padding after the last stream (> 24 KiB)
+static_assert(kJitChunk % (2 * kJitWaves) == 0, "chunk rows split in 2-row pieces over the waves");
+static_assert(kPieces == 6, "register contract: v108-v113");
+static_assert((kJitChunk - 1) * kRowBytes < 65536, "ds_read offset field");
+
+// Rows of one step's chunk and their X slots.
+struct Section {
+    std::vector<int> rows;     // ascending chunk rows used by the wave's columns
+    std::vector<int> slot;     // slot of rows[i]
+    int nblk = 0;
+};
 
 }  // namespace
 
@@ -63,21 +118,69 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     img.N = N;
     img.Npad = ((N + kJitTileCols - 1) / kJitTileCols) * kJitTileCols;
     img.nch = std::max(1, (K + kJitChunk - 1) / kJitChunk);
-    const int nch = img.nch, ntiles = img.Npad / kJitTileCols;
+    const int nch = img.nch, ntiles = img.Npad / kJitTileCols, steps = 2 * nch;
     img.wcode.assign((size_t)ntiles * kJitWaves, 0u);
-    std::vector<uint32_t> &c = img.code;
-    c.clear();
+    std::vector<uint32_t> &code = img.code;
+    code.clear();
     const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
-    c.reserve((size_t)nnz * 4 + (size_t)ntiles * kJitWaves * 2 * nch * 64 + 64);
-    c.insert(c.end(), {kJitMagic0, kJitMagic1, 0u, 0u});
+    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitWaves * (steps * 220 + 64) + kTailPad + 64);
+    code.insert(code.end(), {kJitMagic0, kJitMagic1, 0u, 0u});
+    Emit E{code};
 
     std::vector<int32_t> cur((size_t)kJitNW * 2), end((size_t)kJitNW * 2);
-    std::vector<int> slot_of(kJitChunk);
-    std::vector<int> rows;
+    // rows of step q (chunk q % nch, pass q / nch) for the current pointers
+    auto rows_of = [&](int q, Section &sec) {
+        const int p = q / nch, klo = (q % nch) * kJitChunk, khi = klo + kJitChunk;
+        const int32_t *ri = p ? rin : rip;
+        bool used[kJitChunk] = {};
+        for (int col = 0; col < kJitNW; col++) {
+            const int32_t e = end[(size_t)col * 2 + p];
+            for (int32_t i = cur[(size_t)col * 2 + p]; i < e && ri[i] < khi; i++) used[ri[i] - klo] = true;
+        }
+        sec.rows.clear();
+        for (int r = 0; r < kJitChunk; r++)
+            if (used[r]) sec.rows.push_back(r);
+        sec.nblk = ((int)sec.rows.size() + kBlockRows - 1) / kBlockRows;
+    };
+    int gblk = 0;  // running block count of the stream: block parity = gblk & 1
+    auto assign_slots = [&](Section &sec) {
+        sec.slot.resize(sec.rows.size());
+        for (size_t i = 0; i < sec.rows.size(); i++)
+            sec.slot[i] = ((gblk + (int)(i / kBlockRows)) & 1) * kBlockRows + (int)(i % kBlockRows);
+        gblk += sec.nblk;
+    };
+    auto emit_reads = [&](const Section &sec, int blk, int q) {
+        const uint32_t vb = kLdsBaseV + (uint32_t)(q % 3);
+        const size_t r0 = (size_t)blk * kBlockRows, r1 = std::min(sec.rows.size(), r0 + kBlockRows);
+        for (size_t i = r0; i < r1; i++)
+            E.ds_read_b64(kXSlot0 + 2u * (uint32_t)sec.slot[i], vb, (uint32_t)sec.rows[i] * kRowBytes);
+    };
+    int base_chunk = -1;  // chunk whose base s[84:85] holds
+    auto emit_dma = [&](int q, int w) {  // stage step q's chunk into LDS buffer q % 3
+        const int j = q % nch;
+        if (j == 0) {
+            E.base_reset();
+        } else {
+            if (base_chunk != j - 1) {  // not reached: chunks are staged in order
+                E.base_reset();
+                for (int i = 0; i < j; i++) E.base_next();
+            } else {
+                E.base_next();
+            }
+        }
+        base_chunk = j;
+        E.nop(4);  // SALU-written SGPR base -> VMEM
+        for (int i = 0; i < kPieces; i++) {
+            E.m0_lit((uint32_t)(q % 3) * kBufBytes + (uint32_t)(2 * (w * kPieces + i)) * kRowBytes);
+            E.nop(0);  // M0 -> LDS-DMA
+            E.glds_x4(kDmaOffV + (uint32_t)i);
+        }
+    };
+
     for (int t = 0; t < ntiles; t++) {
         for (int w = 0; w < kJitWaves; w++) {
-            while (c.size() % 64) emit_nop(c);  // 256-B aligned stream start
-            img.wcode[(size_t)t * kJitWaves + w] = (uint32_t)(c.size() * 4);
+            while (code.size() % 64) E.nop();  // 256-B aligned stream start
+            img.wcode[(size_t)t * kJitWaves + w] = E.pos_bytes();
             const int n0 = t * kJitTileCols + w * kJitNW;
             for (int col = 0; col < kJitNW; col++)
                 for (int p = 0; p < 2; p++) {
@@ -86,57 +189,74 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     cur[(size_t)col * 2 + p] = n < N ? cs[n] : 0;
                     end[(size_t)col * 2 + p] = n < N ? cs[n + 1] : 0;
                 }
-            for (int q = 0; q < 2 * nch; q++) {
-                const int p = q / nch, j = q % nch;
+            base_chunk = -1;
+            gblk = 0;
+            E.save_m0();
+            // prologue: steps 0 and 1 staged, landed, visible
+            emit_dma(0, w);
+            emit_dma(1, w);
+            E.wait_vm0();
+            E.barrier();
+            Section sec, next;
+            bool prefetched = false;
+            rows_of(0, sec);
+            assign_slots(sec);
+            for (int q = 0; q < steps; q++) {
+                const int p = q / nch, klo = (q % nch) * kJitChunk;
                 const bool neg = p == 1;
                 const int32_t *ri = p ? rin : rip;
-                const int klo = j * kJitChunk, khi = klo + kJitChunk;
-                const uint32_t vb = (q & 1) ? kLdsBase1 : kLdsBase0;
-                // rows of this chunk any of the wave's columns uses
-                bool used[kJitChunk] = {};
-                for (int col = 0; col < kJitNW; col++) {
-                    const int32_t e = end[(size_t)col * 2 + p];
-                    for (int32_t i = cur[(size_t)col * 2 + p]; i < e && ri[i] < khi; i++) used[ri[i] - klo] = true;
+                if (q + 2 < steps) emit_dma(q + 2, w);
+                for (uint32_t d = 0; d < 2; d++) {
+                    E.touch_addr(E.pos_bytes() + kTouchAhead + d * 8192u);
+                    E.nop(4);
+                    E.code_touch();
                 }
-                rows.clear();
-                for (int r = 0; r < kJitChunk; r++)
-                    if (used[r]) rows.push_back(r);
-                const int nblk = ((int)rows.size() + kBlockRows - 1) / kBlockRows;
-                for (size_t i = 0; i < rows.size(); i++)
-                    slot_of[rows[i]] = (int)((i / kBlockRows) & 1) * kBlockRows + (int)(i % kBlockRows);
-                auto emit_reads = [&](int blk) {
-                    const size_t r0 = (size_t)blk * kBlockRows, r1 = std::min(rows.size(), r0 + kBlockRows);
-                    for (size_t i = r0; i < r1; i++)
-                        emit_ds_read_b128(c, kXSlot0 + 4u * (uint32_t)slot_of[rows[i]], vb,
-                                          (uint32_t)rows[i] * 1024u);
-                };
-                if (nblk > 0) {
-                    emit_reads(0);
-                    emit_wait_lgkm0(c);
-                    emit_nop(c);  // keeps the 8-byte VOP3P instructions 8-byte aligned
+                if (sec.nblk > 0) {
+                    if (!prefetched) emit_reads(sec, 0, q);
+                    E.wait_lgkm0();
                 }
-                for (int blk = 0; blk < nblk; blk++) {
-                    if (blk + 1 < nblk) emit_reads(blk + 1);
-                    const int rhi = (blk + 1 < nblk) ? rows[(size_t)(blk + 1) * kBlockRows] : kJitChunk;
-                    for (int col = 0; col < kJitNW; col++) {
-                        int32_t &i = cur[(size_t)col * 2 + p];
-                        const int32_t e = end[(size_t)col * 2 + p];
-                        const uint32_t acc = kAcc0 + 4u * (uint32_t)col;
-                        for (; i < e && ri[i] < klo + rhi; i++) {
-                            const uint32_t x = kXSlot0 + 4u * (uint32_t)slot_of[ri[i] - klo];
-                            emit_pk_add(c, acc, x, neg);
-                            emit_pk_add(c, acc + 2, x + 2, neg);
+                for (int blk = 0; blk < sec.nblk; blk++) {
+                    if (blk + 1 < sec.nblk) emit_reads(sec, blk + 1, q);
+                    const int rhi = (blk + 1 < sec.nblk) ? sec.rows[(size_t)(blk + 1) * kBlockRows] : kJitChunk;
+                    // slot of a chunk row within this block
+                    int slot_of[kJitChunk];
+                    for (size_t i = (size_t)blk * kBlockRows; i < sec.rows.size() && sec.rows[i] < rhi; i++)
+                        slot_of[sec.rows[i]] = sec.slot[i];
+                    // columns in pairs, their entries interleaved (two independent
+                    // chains back to back); each column keeps ascending k
+                    for (int col = 0; col < kJitNW; col += 2) {
+                        int32_t &ia = cur[(size_t)col * 2 + p], &ib = cur[(size_t)(col + 1) * 2 + p];
+                        const int32_t ea = end[(size_t)col * 2 + p], eb = end[(size_t)(col + 1) * 2 + p];
+                        const uint32_t acca = kAcc0 + 2u * (uint32_t)col, accb = acca + 2u;
+                        for (;;) {
+                            const bool ha = ia < ea && ri[ia] < klo + rhi, hb = ib < eb && ri[ib] < klo + rhi;
+                            if (!ha && !hb) break;
+                            if (ha) E.pk_add(acca, kXSlot0 + 2u * (uint32_t)slot_of[ri[ia++] - klo], neg);
+                            if (hb) E.pk_add(accb, kXSlot0 + 2u * (uint32_t)slot_of[ri[ib++] - klo], neg);
                         }
                     }
-                    if (blk + 1 < nblk) {
-                        emit_wait_lgkm0(c);
-                        emit_nop(c);
+                    if (blk + 1 < sec.nblk) E.wait_lgkm0();
+                }
+                // next step's first block: its chunk is already resident (staged
+                // two steps ahead), so read it before the barrier
+                prefetched = false;
+                if (q + 1 < steps) {
+                    rows_of(q + 1, next);
+                    assign_slots(next);
+                    if (next.nblk > 0) {
+                        emit_reads(next, 0, q + 1);
+                        prefetched = true;
                     }
                 }
-                emit_return(c);
+                E.wait_vm0();
+                E.barrier();
+                std::swap(sec, next);
             }
+            E.restore_m0();
+            E.ret();
         }
     }
+    for (int i = 0; i < kTailPad; i++) E.nop();  // the code prefetch reads past the last stream
 }
 
 // ------------------------------------------------------------ code object --

@@ -11,21 +11,29 @@
 // indices at run time pays, per nonzero, for the index (LDS gather or
 // register-indexed add) and per column for a data-dependent branch -- the
 // measured cost of the register-X walk was 2-3x its adds.  Here every nonzero
-// of a wave's 32 columns is a v_pk_add_f32 pair whose X register (a row of
-// the current X^T block, loaded by ds_read_b128) and accumulator are encoded
-// in the instruction: no index traffic, no SALU, no branch.  The same code
-// serves every 256-row M tile.
+// of a wave's 64 columns is one v_pk_add_f32 (2 M rows per lane) whose X
+// register (a row of the current X^T block, loaded by ds_read_b64) and
+// accumulator are encoded in the instruction: no index traffic, no SALU, no
+// branch.  The same code serves every 128-row M tile.
 //
-// Workgroup: 256 M rows (4 per lane) x 8 waves x 32 columns, 512 threads, one
-// per CU (2 waves per SIMD).  Step q = p*nch + j (p = 0: +1 entries, p = 1:
-// -1 entries; chunk j of 64 K rows): the chunk is in LDS buffer q&1 (staged
-// by LDS-DMA during step q-1), the wave calls its generated section for step
-// q, then the workgroup barriers.  Register contract with the generator
-// (tsg_jit.cpp): v[8:103] X slots (24 rows x 4 M rows), v104/v105 LDS byte
-// address of lane row 0 in buffer 0/1, v[112:239] accumulators (column c of
-// the wave at v[112+4c : 115+4c]), s[92:93] code pointer, s[94:95] return
-// address.  A section ends with `s_getpc_b64 s[92:93]; s_setpc_b64 s[94:95]`,
-// so the next section starts 4 bytes past the returned pointer.
+// Workgroup: 128 M rows (2 per lane) x 8 waves x 64 columns, 512 threads, one
+// per CU (2 waves per SIMD).  The dispatcher sets up registers and calls the
+// wave's generated stream ONCE; the stream itself runs the whole K loop:
+// X^T chunks of 96 rows in a ring of 3 LDS buffers, each staged by LDS-DMA two
+// steps ahead, one `s_waitcnt vmcnt(0); s_barrier` per step (step q = pass
+// p * nch + chunk j: p = 0 the +1 entries, p = 1 the -1 entries), the next
+// step's first X rows read before the barrier, the stream's own code touched
+// 8-24 KiB ahead (L2 prefetch).  Register contract (tsg_jit.cpp):
+//   v[8:103]    X slots (48 rows x 2 M rows)
+//   v104-v106   LDS byte address of lane row 0 in buffer 0/1/2
+//   v107        code-prefetch sink
+//   v108-v113   per-lane byte offsets (from the chunk base) of this wave's 6
+//               LDS-DMA pieces (2 rows each)
+//   v114        lane * 128 (code prefetch)
+//   v[116:243]  accumulators, column c of the wave at v[116+2c : 117+2c]
+//   s[80:81] X^T base, s82 chunk stride in bytes, s[84:85] chunk base (stream),
+//   s86 saved M0, s[88:89] prefetch address (stream), s[92:93] region base,
+//   s[94:95] return address.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -33,36 +41,12 @@
 namespace {
 
 constexpr int kJWaves = 8;
-constexpr int kJNW = 32;
-constexpr int kJTileM = 256;
-constexpr int kJChunk = 64;
+constexpr int kJNW = 64;
+constexpr int kJTileM = 128;
+constexpr int kJChunk = 96;
+constexpr int kJBufBytes = kJChunk * kJTileM * 4;  // 48 KiB
+constexpr int kJPieces = kJChunk / kJWaves / 2;     // LDS-DMA pieces per wave per chunk
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
-
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst)
-{
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-}
-
-// X^T chunk j (64 rows x 256 M) -> LDS buffer buf: one 1 KiB row per
-// wave-instruction, 8 per wave.
-__device__ __forceinline__ void stage(const float *__restrict__ XT, int Mp, int m0, int j, int buf, int wave,
-                                      int lane)
-{
-#pragma unroll
-    for (int i = 0; i < kJChunk / kJWaves; i++) {
-        const int r = wave * (kJChunk / kJWaves) + i;
-        glds16(XT + (size_t)(j * kJChunk + r) * Mp + m0 + 4 * lane, (uint32_t)(buf * 65536 + r * 1024));
-    }
-}
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 
@@ -74,7 +58,8 @@ typedef float F32x32 __attribute__((ext_vector_type(32)));
         "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73",  \
         "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86",  \
         "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99",  \
-        "v100", "v101", "v102", "v103", "s94", "s95", "scc", "memory"
+        "v100", "v101", "v102", "v103", "v107", "s84", "s85", "s86", "s88", "s89", "s94", "s95",   \
+        "scc", "memory"
 
 }  // namespace
 
@@ -83,10 +68,10 @@ extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
+    __shared__ __attribute__((aligned(16))) char lds[3 * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
-    // LDS is only addressed from asm, at absolute offsets from 0 (the only
-    // LDS object): this use keeps the allocation in the kernel descriptor
+    // LDS is only addressed from the generated code, at absolute offsets from
+    // 0 (the only LDS object): this use keeps the allocation in the descriptor
     asm volatile("; lds %0" ::"v"(lds));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -106,9 +91,9 @@ extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
         return;
     }
 
-    // XCD-aware bijective remap (as the rx kernel): each XCD gets a contiguous
-    // n-tile-major run, so the 16 M tiles of a column tile run together on one
-    // XCD and share its code (and entry-free X^T slab) through that XCD's L2.
+    // XCD-aware bijective remap: each XCD gets a contiguous n-tile-major run,
+    // so the M tiles of a column tile run together on one XCD and share its
+    // code through that XCD's L2.
     const int T = mtiles * ntiles, L = blockIdx.x;
     const int xcd = L & 7, slot = L >> 3, q8 = T >> 3, r8 = T & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
@@ -116,44 +101,43 @@ extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
     const int m0 = mt * kJTileM;
     const int ncol0 = nt * (kJWaves * kJNW) + wave * kJNW;
 
-    uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + wave]);
-    const uint32_t lb0 = (uint32_t)lane * 16u, lb1 = 65536u + (uint32_t)lane * 16u;
-
-    stage(XT, Mp, m0, 0, 0, wave, lane);
-    F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int steps = 2 * nch;
-    for (int q = 0; q < steps; q++) {
-        if (q + 1 < steps) stage(XT, Mp, m0, (q + 1) % nch, (q + 1) & 1, wave, lane);
-        asm volatile("s_getpc_b64 s[94:95]\n"
-                     ".Ljr%=:\n\t"
-                     "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
-                     "s_addc_u32 s95, s95, 0\n\t"
-                     "s_setpc_b64 s[92:93]\n"
-                     ".Ljb%=:\n\t"
-                     "s_add_u32 s92, s92, 4\n\t"
-                     "s_addc_u32 s93, s93, 0"
-                     : "+{v[112:143]}"(a0), "+{v[144:175]}"(a1), "+{v[176:207]}"(a2), "+{v[208:239]}"(a3),
-                       "+{s[92:93]}"(cp)
-                     : "{v104}"(lb0), "{v105}"(lb1)
-                     : TSG_JIT_CLOBBERS);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA for q+1 landed
-        __syncthreads();                                   // ... and every other wave's
+    const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + wave]);
+    const uint32_t lb0 = (uint32_t)lane * 8u, lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
+    // LDS-DMA piece i of this wave: chunk rows 2*(wave*6 + i) + {0: lanes 0-31, 1: lanes 32-63}
+    uint32_t off[kJPieces];
+#pragma unroll
+    for (int i = 0; i < kJPieces; i++) {
+        const uint32_t r = 2u * (uint32_t)(wave * kJPieces + i) + (uint32_t)(lane >> 5);
+        off[i] = (r * (uint32_t)Mp + (uint32_t)m0 + 4u * (uint32_t)(lane & 31)) * 4u;
     }
+    const uint32_t l128 = (uint32_t)lane * 128u;
+    const uint32_t stride = (uint32_t)kJChunk * (uint32_t)Mp * 4u;
+
+    F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
+    asm volatile("s_getpc_b64 s[94:95]\n"
+                 ".Ljr%=:\n\t"
+                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
+                 "s_addc_u32 s95, s95, 0\n\t"
+                 "s_setpc_b64 %[cp]\n"
+                 ".Ljb%=:"
+                 : "+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3)
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{v104}"(lb0),
+                   "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]), "{v110}"(off[2]),
+                   "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                 : TSG_JIT_CLOBBERS);
 
     if (ncol0 >= N) return;
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int m = m0 + 4 * lane + r;
+    for (int r = 0; r < 2; r++) {
+        const int m = m0 + 2 * lane + r;
         if (m >= M) continue;
         float *yrow = Y + (size_t)m * N + ncol0;
         float v[kJNW];
 #pragma unroll
         for (int c = 0; c < kJNW; c++) {
             const int n = ncol0 + c < N ? ncol0 + c : N - 1;
-            const float acc = c < 8 ? a0[4 * (c & 7) + r] : c < 16 ? a1[4 * (c & 7) + r]
-                             : c < 24 ? a2[4 * (c & 7) + r] : a3[4 * (c & 7) + r];
+            const float acc = c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
+                             : c < 48 ? a2[2 * (c & 15) + r] : a3[2 * (c & 15) + r];
             float y = acc + b[n];                        // comp.h:63
             if (prelu) y = (y > 0) ? y : alpha[n] * y;   // comp_prelu.h:57-67
             v[c] = y;

@@ -1,133 +1,197 @@
 """The weight-compiled kernel's machine code, checked on the CPU before any GPU
-runs it: tsg_jit_codegen's region is decoded instruction by instruction (only
-the handful of gfx950 encodings the generator may emit are accepted) and
-emulated against the register contract of ternary-spgemm_amd/csrc/tsg_jit_kernel.hip;
-the emulated Y must equal the BaseTCSC oracle (comp.h:25-69) bit for bit, for
-integer and for order-sensitive non-integer X.  This is the test that says the
-generated code computes BaseTCSC in BaseTCSC's order; tests/test_gpu_parity.py
-then says the GPU runs that code."""
+runs it.  tsg_jit_codegen's region is decoded instruction by instruction (only
+the gfx950 encodings the generator may emit are accepted) and a whole
+workgroup is emulated against the register contract of
+ternary-spgemm_amd/csrc/tsg_jit_kernel.hip: its 8 waves run barrier phase by
+barrier phase, LDS-DMA copies land at the issuing wave's `s_waitcnt vmcnt(0)`,
+and every LDS read is checked to see data that landed in an EARLIER phase (no
+read-after-DMA race) while no DMA may overwrite rows read since it was issued
+(no write-after-read race).  Code-prefetch loads must stay inside the region.
+The emulated Y must equal the BaseTCSC oracle (comp.h:25-69) bit for bit, for
+integer and for order-sensitive non-integer X.  tests/test_gpu_parity.py then
+shows the GPU runs that code."""
 import numpy as np
 import pytest
 
-TILE_M, WAVES, NW, TILE_COLS, CHUNK = 256, 8, 32, 256, 64
+TILE_M, WAVES, NW, CHUNK, NBUF = 128, 8, 64, 96, 3
+TILE_COLS = WAVES * NW
+ROW_BYTES = TILE_M * 4
+BUF_BYTES = CHUNK * ROW_BYTES
+PIECES = CHUNK // WAVES // 2
 MAGIC = (0x7453474A, 0x314A4954)
+XT_BASE = 1 << 40  # fake device address of X^T
 
 
-def _decode(w0, w1=None):
-    """-> (kind, fields, n_words) for one instruction at w0[, w1]."""
-    if w0 == 0xBF800000:
+class Wave:
+    def __init__(self, w, pc):
+        self.w, self.pc = w, pc
+        self.v = np.zeros((256, 64), np.float32)
+        self.m0 = 0x5A5A
+        self.saved_m0 = None
+        self.base = None
+        self.touch = None
+        self.pending = []  # DMA copies not yet landed: (lds_byte, data, issue_phase)
+        self.done = False
+
+
+def _decode(code, pc):
+    w0 = int(code[pc])
+    w1 = int(code[pc + 1]) if pc + 1 < len(code) else None
+    if (w0 & 0xFFFFFFF0) == 0xBF800000:
         return "nop", (), 1
-    if w0 == 0xBF8CC07F:
-        return "wait", (), 1
-    if w0 == 0xBEDC1C00 and w1 == 0xBE801D5E:
-        return "ret", (), 2
+    simple = {0xBF8CC07F: "wait_lgkm", 0xBF8C0F70: "wait_vm", 0xBF8A0000: "barrier", 0xBED6007C: "save_m0",
+              0xBEFC0056: "restore_m0", 0xBED40150: "base_reset", 0xBE801D5E: "ret", 0x82558055: "base_addc",
+              0x8259805D: "touch_addc", 0x80545254: "base_add"}
+    if w0 in simple:
+        return simple[w0], (), 1
+    if w0 == 0xBEFC00FF:
+        return "m0", (w1,), 2
+    if w0 == 0x8058FF5C:
+        return "touch_addr", (w1,), 2
+    if w0 == 0xDC508000:
+        assert w1 == (107 << 24) | (88 << 16) | 114
+        return "touch", (), 2
+    if w0 == 0xDDF48000:
+        assert (w1 >> 16) == 84
+        return "glds", (w1 & 0xFF,), 2
     if (w0 & 0xFFFFFD00) == 0xD3B24000:  # v_pk_add_f32
-        d = w0 & 0xFF
-        neg = bool(w0 & 0x200)
-        src0 = (w1 & 0x1FF) - 256
-        src1 = ((w1 >> 9) & 0x1FF) - 256
-        assert (w1 >> 18) & 0x1FF == 0, "src2 field must be empty"
-        assert (w1 >> 27) & 3 == 3, "op_sel_hi must be [1,1]"
-        assert (w1 >> 29) == (2 if neg else 0), "neg_lo must match neg_hi"
+        d, neg = w0 & 0xFF, bool(w0 & 0x200)
+        src0, src1 = (w1 & 0x1FF) - 256, ((w1 >> 9) & 0x1FF) - 256
+        assert (w1 >> 18) & 0x1FF == 0 and (w1 >> 27) & 3 == 3 and (w1 >> 29) == (2 if neg else 0)
         assert src0 == d, "v_pk_add_f32 must accumulate in place"
+        assert 116 <= d <= 242 and d % 2 == 0 and 8 <= src1 <= 102 and src1 % 2 == 0
         return "add", (d, src1, neg), 2
-    if (w0 & 0xFFFF0000) == 0xD9FE0000:  # ds_read_b128
-        off = w0 & 0xFFFF
-        a, vd = w1 & 0xFF, w1 >> 24
+    if (w0 & 0xFFFF0000) == 0xD8EC0000:  # ds_read_b64
         assert (w1 >> 8) & 0xFFFF == 0
-        return "read", (vd, a, off), 2
-    raise AssertionError(f"unexpected instruction word {w0:#010x}")
+        return "read", (w1 >> 24, w1 & 0xFF, w0 & 0xFFFF), 2
+    raise AssertionError(f"unexpected instruction word {w0:#010x} at word {pc}")
 
 
-def emulate(code, wcode, XT, M, K, N, nch):
-    """Runs every (tile, wave) stream on the data a workgroup would see."""
-    assert tuple(code[:2]) == MAGIC
-    Mp = XT.shape[1]
-    ntiles = len(wcode) // WAVES
-    acc_out = np.zeros((Mp, ntiles * TILE_COLS), np.float32)
-    for t in range(ntiles):
-        for w in range(WAVES):
-            for mt in range(Mp // TILE_M):
-                m0 = mt * TILE_M
-                v = np.zeros((256, 64), np.float32)  # VGPR file, one column per lane
-                pc = int(wcode[t * WAVES + w]) // 4
-                assert int(wcode[t * WAVES + w]) % 256 == 0
-                for q in range(2 * nch):
-                    j = q % nch
-                    chunk = XT[j * CHUNK:(j + 1) * CHUNK, m0:m0 + TILE_M]  # [row][m]
-                    while True:
-                        kind, f, nw = _decode(int(code[pc]), int(code[pc + 1]) if pc + 1 < len(code) else None)
-                        pc += nw
-                        if kind == "ret":
-                            break
-                        if kind == "read":
-                            vd, a, off = f
-                            assert a == (105 if q & 1 else 104), "read from the wrong LDS buffer"
-                            assert off % 1024 == 0 and off // 1024 < CHUNK
-                            assert 8 <= vd and vd + 3 <= 103 and (vd - 8) % 4 == 0
-                            row = chunk[off // 1024]  # 256 M values; lane l gets 4l..4l+3
-                            v[vd:vd + 4] = row.reshape(64, 4).T
-                        elif kind == "add":
-                            d, x, neg = f
-                            assert 112 <= d <= 238 and 8 <= x <= 102
-                            if neg:
-                                v[d:d + 2] = v[d:d + 2] - v[x:x + 2]
-                            else:
-                                v[d:d + 2] = v[d:d + 2] + v[x:x + 2]
-                    # the dispatcher resumes 4 bytes past the s_setpc
-                    pc = pc  # (pc already points past the 2-word return pair)
-                n0 = t * TILE_COLS + w * NW
-                for c in range(NW):
-                    for i in range(4):
-                        acc_out[m0 + i:m0 + TILE_M:4, n0 + c] = v[112 + 4 * c + i]
-    return acc_out[:M, :N]
+def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
+    """One workgroup (column tile t, M tile at m0): returns acc[128 rows, 512 cols]."""
+    region_bytes = len(code) * 4
+    stride = CHUNK * Mp * 4
+    lanes = np.arange(64)
+    lds = np.zeros(NBUF * BUF_BYTES // 4, np.float32)
+    landed = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)   # phase a row's data landed
+    last_read = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)
+    waves = [Wave(w, int(wcode[t * WAVES + w]) // 4) for w in range(WAVES)]
+    for wv in waves:
+        assert int(wcode[t * WAVES + wv.w]) % 256 == 0
+    phase = 0
+    while not all(wv.done for wv in waves):
+        at_barrier = 0
+        for wv in waves:
+            if wv.done:
+                continue
+            while True:
+                kind, f, n = _decode(code, wv.pc)
+                wv.pc += n
+                if kind == "barrier":
+                    at_barrier += 1
+                    break
+                if kind == "ret":
+                    assert not wv.pending and wv.m0 == 0x5A5A
+                    wv.done = True
+                    break
+                if kind == "save_m0":
+                    wv.saved_m0 = wv.m0
+                elif kind == "restore_m0":
+                    wv.m0 = wv.saved_m0
+                elif kind == "m0":
+                    wv.m0 = f[0]
+                elif kind == "base_reset":
+                    wv.base = XT_BASE
+                elif kind == "base_add":
+                    wv.base += stride
+                elif kind == "touch_addr":
+                    wv.touch = f[0]
+                elif kind == "touch":
+                    assert wv.touch is not None and wv.touch + 63 * 128 + 4 <= region_bytes, "prefetch past region"
+                elif kind == "glds":
+                    i = f[0] - 108
+                    assert 0 <= i < PIECES
+                    chunk_row0 = 2 * (wv.w * PIECES + i)
+                    j, rem = divmod(wv.base - XT_BASE, stride)
+                    assert rem == 0 and 0 <= j < nch
+                    assert wv.m0 % BUF_BYTES == chunk_row0 * ROW_BYTES, "DMA lands on the wrong rows"
+                    for half in range(2):
+                        src = XT[j * CHUNK + chunk_row0 + half, m0:m0 + TILE_M]
+                        wv.pending.append((wv.m0 + half * ROW_BYTES, src.copy(), phase))
+                elif kind == "wait_vm":
+                    for dst, data, iss in wv.pending:
+                        row = dst // ROW_BYTES
+                        assert last_read[row] < iss, "DMA overwrites a row read since its issue (WAR race)"
+                        lds[dst // 4:dst // 4 + TILE_M] = data
+                        landed[row] = phase
+                    wv.pending = []
+                elif kind == "read":
+                    vd, a, off = f
+                    assert 104 <= a <= 106 and off % ROW_BYTES == 0 and off // ROW_BYTES < CHUNK
+                    row = (a - 104) * CHUNK + off // ROW_BYTES
+                    assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
+                    last_read[row] = max(last_read[row], phase)
+                    vals = lds[row * TILE_M:(row + 1) * TILE_M]
+                    wv.v[vd:vd + 2] = vals.reshape(64, 2).T
+                elif kind == "add":
+                    d, x, neg = f
+                    wv.v[d:d + 2] = wv.v[d:d + 2] - wv.v[x:x + 2] if neg else wv.v[d:d + 2] + wv.v[x:x + 2]
+        assert at_barrier in (0, WAVES), "waves disagree on the barrier count"
+        phase += 1
+    acc = np.zeros((TILE_M, TILE_COLS), np.float32)
+    for wv in waves:
+        for c in range(NW):
+            for r in range(2):
+                acc[r::2, wv.w * NW + c] = wv.v[116 + 2 * c + r]
+    return acc
 
 
-def _check(tsg, O, M, K, N, s, seed, frac):
-    W = O.gen_ternary(K, N, s, seed)
-    t = O.tcsc_encode(W)
-    code, wcode = tsg.jit_codegen(*t.arrays, K, N)
+def emulate(code, wcode, X, K, N):
+    assert tuple(int(x) for x in code[:2]) == MAGIC
+    M = X.shape[0]
     nch = max(1, -(-K // CHUNK))
     Mp = -(-max(M, 1) // TILE_M) * TILE_M
-    X = O.init_x_frac(M, K, seed + 1) if frac else O.init_x_int(M, K, seed + 1)
     XT = np.zeros((nch * CHUNK, Mp), np.float32)
     XT[:K, :M] = X.T
+    ntiles = len(wcode) // WAVES
+    Y = np.zeros((Mp, ntiles * TILE_COLS), np.float32)
+    for t in range(ntiles):
+        for m0 in range(0, Mp, TILE_M):
+            Y[m0:m0 + TILE_M, t * TILE_COLS:(t + 1) * TILE_COLS] = emulate_tile(code, wcode, t, XT, m0, Mp, nch)
+    return Y[:M, :N]
+
+
+def _check(tsg, O, M, K, N, s, seed, frac, W=None):
+    W = O.gen_ternary(K, N, s, seed) if W is None else W
+    t = O.tcsc_encode(W)
+    code, wcode = tsg.jit_codegen(*t.arrays, K, N)
+    X = O.init_x_frac(M, K, seed + 1) if frac else O.init_x_int(M, K, seed + 1)
     b = np.linspace(-2, 3, N).astype(np.float32)
-    Y = emulate(code, wcode, XT, M, K, N, nch) + b
+    Y = emulate(code, wcode, X, K, N) + b
     ref = O.base_tcsc(X, t, b)
     assert np.array_equal(Y.view(np.uint32), ref.view(np.uint32)), (M, K, N, s, frac)
-    # one v_pk_add_f32 pair per nonzero, nothing else that adds
-    n_add = sum(1 for i in range(len(code) - 1) if (int(code[i]) & 0xFFFFFD00) == 0xD3B24000)
-    assert n_add == 2 * (len(t.arrays[2]) + len(t.arrays[3]))
+    # one v_pk_add_f32 per nonzero, nothing else that adds
+    n_add = sum(1 for i in range(len(code) - 1) if (int(code[i]) & 0xFFFFFD00) == 0xD3B24000
+                and (int(code[i + 1]) >> 27) & 3 == 3)
+    assert n_add == len(t.arrays[2]) + len(t.arrays[3])
 
 
-@pytest.mark.parametrize("M,K,N,s", [(1, 1, 1, 1), (5, 70, 33, 2), (256, 130, 300, 4), (300, 64, 257, 8),
-                                     (17, 200, 40, 16), (3, 0, 9, 4)])
+@pytest.mark.parametrize("M,K,N,s", [(1, 1, 1, 1), (5, 70, 33, 2), (130, 200, 520, 4), (17, 300, 64, 8),
+                                     (3, 97, 9, 16)])
 def test_jit_code_emulates_base_tcsc(tsg, oracle_mod, M, K, N, s):
     for frac in (False, True):
-        if K == 0:
-            continue
         _check(tsg, oracle_mod, M, K, N, s, 11 + K + N, frac)
 
 
 def test_jit_code_dense_and_empty_columns(tsg, oracle_mod):
-    """All-+1 / all--1 / empty columns: 64 entries per chunk in one column, more
-    rows than one X block holds, and streams with no entries at all."""
+    """All-+1 / all--1 / alternating / empty columns: every row of a chunk used,
+    more rows than one X block holds, and streams with no entries at all."""
     O = oracle_mod
-    K, N, M = 150, 40, 9
+    K, N, M = 250, 40, 9
     W = np.zeros((K, N), np.int32)
     W[:, 0] = 1
     W[:, 1] = -1
     W[::2, 2] = 1
     W[1::2, 2] = -1
     W[:, 5:] = O.gen_ternary(K, N - 5, 2, 3)
-    t = O.tcsc_encode(W)
-    code, wcode = tsg.jit_codegen(*t.arrays, K, N)
-    nch = -(-K // CHUNK)
-    X = O.init_x_frac(M, K, 4)
-    XT = np.zeros((nch * CHUNK, TILE_M), np.float32)
-    XT[:K, :M] = X.T
-    b = np.zeros(N, np.float32)
-    Y = emulate(code, wcode, XT, M, K, N, nch) + b
-    ref = O.base_tcsc(X, t, b)
-    assert np.array_equal(Y.view(np.uint32), ref.view(np.uint32))
+    _check(tsg, O, M, K, N, 0, 4, True, W=W)
