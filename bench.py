@@ -31,10 +31,10 @@ import tsg_dist as D  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
 PROFILE_PMC = os.path.join(REPO, "profiles", "r01_pmc_summary.json")
-# LDS read roof of the stream kernel: 256 B/clk/CU (ds_read_b64, MI355X_MICROARCH.md
-# LDS table) x 256 CUs x 2.4 GHz.  Every (nonzero, 128-row tile) costs one 512-B
-# ds_read_b64 wave-instruction.
-LDS_PEAK_TBPS = 256 * 256 * 2.4e9 / 1e12
+# Binding roof of the path: fp32 VALU adds.  v_pk_add_f32 retires 2 IEEE adds per
+# lane, 128 adds/clk/CU (measured 121 in scripts/issue_micro.hip), x 256 CUs x
+# 2.4 GHz = 78.6 T adds/s (the 157.3 TFLOP/s fp32 vector spec counts an FMA as 2).
+VALU_PEAK_TADDS = 128 * 256 * 2.4e9 / 1e12
 
 
 def parse():
@@ -78,6 +78,7 @@ def main():
     t0 = time.time()
     csp, csn, rip, rin = T.gen_tcsc(K, Ntot, s, a.seed_w, n0, n1)
     h = T.TCSCDevice(csp, csn, rip, rin, K, Nr, device=local)
+    kname = h.kernel_name()
     nnz = int(len(rip) + len(rin))
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed_x)
@@ -158,13 +159,14 @@ def main():
         value = flops_all * a.steps / elapsed_max / 1e9
         ms_step = elapsed_max / a.steps * 1e3
         alg_bytes = T.algorithmic_bytes(M, Nr, K, nnz)  # per launch, this rank
-        lds_bytes = ((M + 127) // 128) * nnz * 512       # LDS bytes the gathers must read
+        adds = T.flops(M, Nr, nnz)                       # per launch: one IEEE add per (m, nonzero) + bias
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
         traffic = None
         try:
             pm = json.load(open(PROFILE_PMC))
             key = f"{M}x{K}x{Nr}s{s}"
-            traffic = pm.get("per_launch_hbm_bytes", {}).get(key)
+            if pm.get("kernel") == kname:
+                traffic = pm.get("per_launch_hbm_bytes", {}).get(key)
         except Exception:
             pass
         out = {
@@ -188,15 +190,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic,
-                         "kernel": "tsg_tcsc_stream_kernel", "kernel_ms": round(kern_ms_max, 4),
+                         "kernel": kname, "kernel_ms": round(kern_ms_max, 4),
                          "algorithmic_bytes_per_launch": alg_bytes,
-                         "kernel_gflops": round(T.flops(M, Nr, nnz) / (kern_ms_max * 1e-3) / 1e9, 2),
-                         "traffic_source": (PROFILE_PMC if traffic is not None else None),
-                         "lds": {"bound_for": "stream kernel at this M (DESIGN.md 5)",
-                                 "algorithmic_bytes": lds_bytes,
-                                 "achieved_TBps": round(lds_bytes / (kern_ms_max * 1e-3) / 1e12, 2),
-                                 "peak_TBps": round(LDS_PEAK_TBPS, 1),
-                                 "frac": round(lds_bytes / (kern_ms_max * 1e-3) / 1e12 / LDS_PEAK_TBPS, 4)}},
+                         "kernel_gflops": round(adds / (kern_ms_max * 1e-3) / 1e9, 2),
+                         "traffic_source": (os.path.relpath(PROFILE_PMC, REPO) if traffic is not None else None),
+                         "binding": {"resource": "valu fp32 adds (DESIGN.md 5)", "adds_per_launch": adds,
+                                     "achieved_Tadds": round(adds / (kern_ms_max * 1e-3) / 1e12, 2),
+                                     "peak_Tadds": round(VALU_PEAK_TADDS, 2),
+                                     "frac": round(adds / (kern_ms_max * 1e-3) / 1e12 / VALU_PEAK_TADDS, 4)}},
             "cpu_baseline": cpu,
             "stream_ms_per_step": round(stream_ms / a.steps, 4),
             "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),

@@ -112,6 +112,11 @@ int tcsc_hip_to_dense(const tsg_tcsc *h, int32_t *W, int K, int N);
 int tcsc_hip_set_timing(tsg_tcsc *h, int enable);
 int tcsc_hip_kernel_time(tsg_tcsc *h, double *total_ms, int64_t *launches, int reset);
 
+/* Name of the device kernel this handle launches (the one timed above):
+ * "tsg_jit_kernel" (default: W compiled into gfx950 code at registration) or,
+ * when TSG_KERNEL selects another family at registration, that kernel. */
+const char *tcsc_hip_kernel_name(const tsg_tcsc *h);
+
 const char *tcsc_hip_last_error(void);
 int tcsc_hip_device_count(int *count);
 

@@ -43,7 +43,7 @@ for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")))
         kn = k.split("(")[0].replace("void ", "").strip()
         tot[kn][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[kn][r["Counter_Name"]].add(r["Dispatch_Id"])
-out = {"workload": f"{M}x{K}x{N}s{s}", "kernels": {}, "per_launch_hbm_bytes": {}}
+out = {"workload": f"{M}x{K}x{N}s{s}", "kernel": None, "kernels": {}, "per_launch_hbm_bytes": {}}
 for kn, v in tot.items():
     per = {c: x / max(len(disp[kn][c]), 1) for c, x in v.items()}
     o = {"per_launch": per}
@@ -56,7 +56,9 @@ for kn, v in tot.items():
     if "SQ_LDS_IDX_ACTIVE" in per and "GRBM_GUI_ACTIVE" in per:
         o["lds_util"] = per["SQ_LDS_IDX_ACTIVE"] / (per["GRBM_GUI_ACTIVE"] / 8 * 256)
     out["kernels"][kn] = o
-    if "stream_kernel" in kn and "hbm_bytes" in o:
+    main = kn.split("::")[-1].split("<")[0]
+    if main != "tsg_transpose_kernel" and "hbm_bytes" in o:  # the TCSC kernel
+        out["kernel"] = main
         out["per_launch_hbm_bytes"][out["workload"]] = o["hbm_bytes"]
 json.dump(out, open(dst + "_pmc_summary.json", "w"), indent=1)
 print(json.dumps(out, indent=1)[:3000])

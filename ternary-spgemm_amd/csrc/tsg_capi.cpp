@@ -324,13 +324,18 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     h->csn.assign(csn, csn + N + 1);
     if (h->nnz_pos) h->rip.assign(rip, rip + h->nnz_pos);
     if (h->nnz_neg) h->rin.assign(rin, rin + h->nnz_neg);
+    // kernel family (default: the weight-compiled kernel); TSG_KERNEL selects
+    // the others for A/B and their own tests
     const char *kenv = std::getenv("TSG_KERNEL");
-    const bool want_rx = kenv && std::strcmp(kenv, "rx") == 0;
-    const bool want_jit = kenv && std::strcmp(kenv, "jit") == 0;
-    h->kind = want_jit ? tsg_tcsc::kJit
-              : want_rx ? tsg_tcsc::kRx
-              : (kenv && std::strcmp(kenv, "chunked") == 0) ? tsg_tcsc::kChunked
-                                                             : tsg_tcsc::kStream;
+    const std::string kname = kenv ? kenv : "jit";
+    if (kname == "jit") h->kind = tsg_tcsc::kJit;
+    else if (kname == "rx") h->kind = tsg_tcsc::kRx;
+    else if (kname == "chunked") h->kind = tsg_tcsc::kChunked;
+    else if (kname == "stream" || kname == "pair" || kname == "flat") h->kind = tsg_tcsc::kStream;
+    else {
+        delete h;
+        return fail(TSG_ERR_ARG, "TSG_KERNEL=" + kname + ": expected jit, rx, stream, pair, flat or chunked");
+    }
     h->stream_kernel = h->kind == tsg_tcsc::kStream;
     const std::vector<uint32_t> *segv, *entv;
     static const std::vector<uint32_t> kNoEntries(1, 0u);
@@ -344,10 +349,16 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
             free_handle(h);
             return fail(TSG_ERR_HIP, "jit kernel: " + err);
         }
-        if (const char *d = std::getenv("TSG_JIT_DIAG"))  // diagnostic: every tile runs tile 0's code
-            if (std::strcmp(d, "samecode") == 0)
+        if (const char *d = std::getenv("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
+            if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
                 for (size_t i = tsg::kJitWaves; i < h->jimg.wcode.size(); i++)
                     h->jimg.wcode[i] = h->jimg.wcode[i % tsg::kJitWaves];
+            if (std::strstr(d, "samewave"))  // every wave of a tile runs its wave 0's stream
+                for (size_t i = 0; i < h->jimg.wcode.size(); i++)
+                    h->jimg.wcode[i] = h->jimg.wcode[i - i % tsg::kJitWaves];
+            if (std::strstr(d, "pairwave"))  // waves 2i and 2i+1 share a stream
+                for (size_t i = 0; i < h->jimg.wcode.size(); i++) h->jimg.wcode[i] = h->jimg.wcode[i & ~(size_t)1];
+        }
         segv = &h->jimg.wcode;
         entv = &kNoEntries;
     } else if (h->kind == tsg_tcsc::kRx) {
@@ -355,8 +366,7 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
         segv = &h->rimg.wstart;
         entv = &h->rimg.ent;
     } else if (h->stream_kernel) {
-        tsg::plan_stream_image(csp, csn, rip, rin, K, N, kenv && std::strcmp(kenv, "flat") == 0,
-                               h->simg);
+        tsg::plan_stream_image(csp, csn, rip, rin, K, N, kname == "flat", h->simg);
         segv = &h->simg.wstart;
         entv = &h->simg.ent;
     } else {
@@ -480,6 +490,17 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     o->tile_rows = jit ? tsg::kJitTileM : rx ? tsg::kRxTileM : tsg::kTileM;
     o->tile_cols = jit ? tsg::kJitTileCols : rx ? tsg::kRxTileCols : h->stream_kernel ? h->simg.tile_cols : h->img.tile_cols;
     return TSG_OK;
+}
+
+extern "C" const char *tcsc_hip_kernel_name(const tsg_tcsc *h)
+{
+    if (!h) return "";
+    switch (h->kind) {
+    case tsg_tcsc::kJit: return "tsg_jit_kernel";
+    case tsg_tcsc::kRx: return "tsg_tcsc_rx_kernel";
+    case tsg_tcsc::kStream: return "tsg_tcsc_stream_kernel";
+    default: return "tsg_tcsc_lds_kernel";
+    }
 }
 
 extern "C" int tcsc_hip_to_dense(const tsg_tcsc *h, int32_t *W, int K, int N)

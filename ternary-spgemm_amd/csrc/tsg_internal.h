@@ -115,14 +115,20 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 // ---------------------------------------------------------------------------
 // "jit" (weight-compiled) kernel: dispatcher tsg_jit_kernel (tsg_jit_kernel.hip,
 // built as the code object lib/tsg_jit.co) + machine code generated from the
-// TCSC arrays (tsg_jit.cpp).  Workgroup: 128 M rows (2 per lane) x 8 waves x
-// 64 columns; X^T chunks of 96 K rows in a ring of 3 LDS buffers (144 KiB).
+// TCSC arrays (tsg_jit.cpp).  Workgroup: 128 M rows (2 per lane) x W waves x
+// NW columns; X^T chunks of 96 K rows in a ring of 3 LDS buffers (144 KiB).
+// Geometry (compile time, TSG_JIT_GEOM, shared with tsg_jit_kernel.hip):
+//   1 (default): 8 waves x 64 columns, 48 X slots, 2 waves per SIMD
+//   2:          16 waves x 32 columns, 24 X slots, 4 waves per SIMD
+#ifndef TSG_JIT_GEOM
+#define TSG_JIT_GEOM 1
+#endif
 constexpr int kJitTileM = 128;
-constexpr int kJitWaves = 8;
-constexpr int kJitNW = 64;
+constexpr int kJitWaves = TSG_JIT_GEOM == 1 ? 8 : 16;
+constexpr int kJitNW = TSG_JIT_GEOM == 1 ? 64 : 32;
 constexpr int kJitTileCols = kJitWaves * kJitNW;
 constexpr int kJitChunk = 96;
-constexpr int kJitSlots = 48;   // X slot registers v[8:103], 2 per slot
+constexpr int kJitSlots = TSG_JIT_GEOM == 1 ? 48 : 24;  // X slot registers v[8 : 8 + 2 * slots)
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
 
 struct JitImage {

@@ -16,6 +16,8 @@
 #include <elf.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iterator>
@@ -57,12 +59,12 @@ struct Emit {
         c.push_back(0xddf48000u);
         c.push_back((84u << 16) | voff);
     }
-    // global_load_dword v107, v114, s[88:89]   (code prefetch into L2)
-    void code_touch()
+    // global_load_dword v[sink], v[lane*128], s[88:89]   (code prefetch into L2)
+    void code_touch(uint32_t sink, uint32_t l128)
     {
         align8();
         c.push_back(0xdc508000u);
-        c.push_back((107u << 24) | (88u << 16) | 114u);
+        c.push_back((sink << 24) | (88u << 16) | l128);
     }
     void m0_lit(uint32_t v) { align8(); c.push_back(0xbefc00ffu); c.push_back(v); }  // s_mov_b32 m0, v
     void save_m0() { c.push_back(0xbed6007cu); }      // s_mov_b32 s86, m0
@@ -81,32 +83,35 @@ struct Emit {
         c.push_back(0x8259805du);
     }
     void nop(uint32_t n = 0) { c.push_back(0xbf800000u | n); }
-    void wait_lgkm0() { c.push_back(0xbf8cc07fu); }
+    void wait_lgkm(uint32_t n) { c.push_back(0xbf8cc07fu | (n << 8)); }  // s_waitcnt lgkmcnt(n), n <= 15
     void wait_vm0() { c.push_back(0xbf8c0f70u); }
     void barrier() { c.push_back(0xbf8a0000u); }
     void ret() { c.push_back(0xbe801d5eu); }         // s_setpc_b64 s[94:95]
     uint32_t pos_bytes() const { return (uint32_t)(c.size() * 4); }
 };
 
-constexpr uint32_t kXSlot0 = 8;          // v[8 + 2s : 9 + 2s], s < kJitSlots
-constexpr uint32_t kLdsBaseV = 104;      // v104 + b: lane row 0 of LDS buffer b
-constexpr uint32_t kDmaOffV = 108;       // v108 + i: DMA piece i offsets
-constexpr uint32_t kAcc0 = 116;          // column c: v[116 + 2c : 117 + 2c]
-constexpr int kBlockRows = kJitSlots / 2;  // double-buffered X row blocks
+// Register contract (tsg_jit_kernel.hip): X slots v[8 : 8 + 2S), then 3 LDS
+// buffer bases, the code-prefetch sink, the DMA piece offsets, lane*128, and
+// the accumulators from the next even register.
+constexpr int kPieces = kJitChunk / kJitWaves / 2;        // DMA pieces per wave per chunk
+constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 2s : 9 + 2s]
+constexpr uint32_t kLdsBaseV = kXSlot0 + 2 * kJitSlots;   // + b: lane row 0 of LDS buffer b
+constexpr uint32_t kSinkV = kLdsBaseV + 3;
+constexpr uint32_t kDmaOffV = kSinkV + 1;                  // + i: DMA piece i offsets
+constexpr uint32_t kLane128V = kDmaOffV + kPieces;
+constexpr uint32_t kAcc0 = (kLane128V + 2) & ~1u;         // column c: v[acc0 + 2c : acc0 + 2c + 1]
+static_assert(kAcc0 + 2 * kJitNW <= (TSG_JIT_GEOM == 1 ? 256u : 128u), "VGPR budget");
 constexpr uint32_t kRowBytes = kJitTileM * 4;             // one X^T row of the tile in LDS
 constexpr uint32_t kBufBytes = kJitChunk * kRowBytes;     // one LDS chunk buffer
-constexpr int kPieces = kJitChunk / kJitWaves / 2;        // DMA pieces per wave per chunk
-constexpr uint32_t kTouchAhead = 8192;   // code prefetch window [pos + 8 KiB, pos + 24 KiB)
-constexpr int kTailPad = 8192 + 1024;    // words of padding after the last stream (> 24 KiB)
+constexpr int kTailPad = 32768 + 1024;   // words of padding after the last stream (code prefetch reads ahead)
 static_assert(kJitChunk % (2 * kJitWaves) == 0, "chunk rows split in 2-row pieces over the waves");
-static_assert(kPieces == 6, "register contract: v108-v113");
 static_assert((kJitChunk - 1) * kRowBytes < 65536, "ds_read offset field");
 
-// Rows of one step's chunk and their X slots.
+// One step's work for a wave: the chunk rows its columns use, ascending, and
+// per row the columns with an entry there (pos or neg pass of the step).
 struct Section {
-    std::vector<int> rows;     // ascending chunk rows used by the wave's columns
-    std::vector<int> slot;     // slot of rows[i]
-    int nblk = 0;
+    std::vector<int> rows;
+    std::vector<std::vector<uint8_t>> cols;
 };
 
 }  // namespace
@@ -124,39 +129,45 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     code.clear();
     const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
     code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitWaves * (steps * 220 + 64) + kTailPad + 64);
-    code.insert(code.end(), {kJitMagic0, kJitMagic1, 0u, 0u});
+    // header: magic, then the geometry (tests/test_jit_codegen.py derives the
+    // register contract from it)
+    code.insert(code.end(), {kJitMagic0, kJitMagic1,
+                             (uint32_t)kJitWaves | (uint32_t)kJitNW << 8 | (uint32_t)kJitChunk << 16,
+                             (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16});
     Emit E{code};
+    // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
+    // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
+    // prefetch), nolgkm (no LDS waits), noreads (no X reads)
+    const std::string diag = std::getenv("TSG_JIT_DIAG") ? std::getenv("TSG_JIT_DIAG") : "";
+    auto has = [&](const char *f) { return diag.find(f) != std::string::npos; };
+    const bool d_nobar = has("nobar"), d_nodma = has("nodma"), d_notouch = has("notouch"),
+               d_nolgkm = has("nolgkm"), d_noreads = has("noreads");
+    // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,2)
+    uint32_t touch_first = 1, touch_count = 2;
+    if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
 
     std::vector<int32_t> cur((size_t)kJitNW * 2), end((size_t)kJitNW * 2);
-    // rows of step q (chunk q % nch, pass q / nch) for the current pointers
-    auto rows_of = [&](int q, Section &sec) {
+    // step q's section: consumes the wave's entries of chunk q % nch, pass q / nch
+    auto build_section = [&](int q, Section &sec) {
         const int p = q / nch, klo = (q % nch) * kJitChunk, khi = klo + kJitChunk;
         const int32_t *ri = p ? rin : rip;
-        bool used[kJitChunk] = {};
+        std::vector<std::vector<uint8_t>> by_row(kJitChunk);
         for (int col = 0; col < kJitNW; col++) {
+            int32_t &i = cur[(size_t)col * 2 + p];
             const int32_t e = end[(size_t)col * 2 + p];
-            for (int32_t i = cur[(size_t)col * 2 + p]; i < e && ri[i] < khi; i++) used[ri[i] - klo] = true;
+            for (; i < e && ri[i] < khi; i++) by_row[ri[i] - klo].push_back((uint8_t)col);
         }
         sec.rows.clear();
+        sec.cols.clear();
         for (int r = 0; r < kJitChunk; r++)
-            if (used[r]) sec.rows.push_back(r);
-        sec.nblk = ((int)sec.rows.size() + kBlockRows - 1) / kBlockRows;
-    };
-    int gblk = 0;  // running block count of the stream: block parity = gblk & 1
-    auto assign_slots = [&](Section &sec) {
-        sec.slot.resize(sec.rows.size());
-        for (size_t i = 0; i < sec.rows.size(); i++)
-            sec.slot[i] = ((gblk + (int)(i / kBlockRows)) & 1) * kBlockRows + (int)(i % kBlockRows);
-        gblk += sec.nblk;
-    };
-    auto emit_reads = [&](const Section &sec, int blk, int q) {
-        const uint32_t vb = kLdsBaseV + (uint32_t)(q % 3);
-        const size_t r0 = (size_t)blk * kBlockRows, r1 = std::min(sec.rows.size(), r0 + kBlockRows);
-        for (size_t i = r0; i < r1; i++)
-            E.ds_read_b64(kXSlot0 + 2u * (uint32_t)sec.slot[i], vb, (uint32_t)sec.rows[i] * kRowBytes);
+            if (!by_row[r].empty()) {
+                sec.rows.push_back(r);
+                sec.cols.push_back(std::move(by_row[r]));
+            }
     };
     int base_chunk = -1;  // chunk whose base s[84:85] holds
     auto emit_dma = [&](int q, int w) {  // stage step q's chunk into LDS buffer q % 3
+        if (d_nodma) return;
         const int j = q % nch;
         if (j == 0) {
             E.base_reset();
@@ -177,6 +188,22 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         }
     };
 
+    // X row schedule.  The wave's used rows, over all steps, form one sequence
+    // g = 0, 1, ...; row g lives in X slot g % kJitSlots.  Rows are processed
+    // in groups of G (never across a step): at a group's start the wave waits
+    // (counted lgkmcnt; LDS returns in order) for the group's reads, then
+    // issues the reads of the following rows up to RA rows past the group (at
+    // most into the next step, whose chunk is already resident), then adds the
+    // group's entries -- column by column (pairs interleaved) or row by row.
+    // Every column meets its rows in ascending k either way.
+    // TSG_JIT_READS="G,RA,order" (order 0 = column-major, 1 = row-major);
+    // default 24,24,0 (the block schedule: one group of reads in flight).
+    int G = kJitSlots / 2, RA = kJitSlots / 2, row_major = 0;
+    if (const char *rv = std::getenv("TSG_JIT_READS")) std::sscanf(rv, "%d,%d,%d", &G, &RA, &row_major);
+    if (G < 1 || RA < 0 || G + RA > kJitSlots) {
+        G = kJitSlots / 2;
+        RA = kJitSlots / 2;
+    }
     for (int t = 0; t < ntiles; t++) {
         for (int w = 0; w < kJitWaves; w++) {
             while (code.size() % 64) E.nop();  // 256-B aligned stream start
@@ -190,67 +217,82 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     end[(size_t)col * 2 + p] = n < N ? cs[n + 1] : 0;
                 }
             base_chunk = -1;
-            gblk = 0;
             E.save_m0();
             // prologue: steps 0 and 1 staged, landed, visible
             emit_dma(0, w);
             emit_dma(1, w);
             E.wait_vm0();
             E.barrier();
-            Section sec, next;
-            bool prefetched = false;
-            rows_of(0, sec);
-            assign_slots(sec);
+            std::vector<Section> secs(steps);
+            std::vector<int64_t> first(steps + 1, 0);  // global index of each step's first row
+            int built = 0;
+            auto ensure = [&](int q) {
+                while (built <= q && built < steps) {
+                    build_section(built, secs[built]);
+                    first[built + 1] = first[built] + (int64_t)secs[built].rows.size();
+                    built++;
+                }
+            };
+            int64_t issued = 0, ready = 0;  // reads issued / reads known complete
+            int rq = 0;                      // step of row `issued`
+            // issue reads up to row `upto` (exclusive), not past step `qmax`
+            auto issue_reads = [&](int64_t upto, int qmax) {
+                qmax = std::min(qmax, steps - 1);
+                for (; issued < upto; issued++) {
+                    while (rq + 1 <= qmax && issued >= first[rq + 1]) rq++;
+                    if (issued >= first[rq + 1]) return;  // past step qmax
+                    const int r = secs[rq].rows[(size_t)(issued - first[rq])];
+                    if (!d_noreads)
+                        E.ds_read_b64(kXSlot0 + 2u * (uint32_t)(issued % kJitSlots), kLdsBaseV + (uint32_t)(rq % 3),
+                                      (uint32_t)r * kRowBytes);
+                }
+            };
+            auto wait_rows = [&](int64_t upto) {  // rows < upto complete
+                if (ready >= upto) return;
+                const int64_t n = std::min<int64_t>(std::max<int64_t>(issued - upto, 0), 15);
+                if (!d_nolgkm) E.wait_lgkm((uint32_t)n);
+                ready = issued - n;
+            };
             for (int q = 0; q < steps; q++) {
-                const int p = q / nch, klo = (q % nch) * kJitChunk;
-                const bool neg = p == 1;
-                const int32_t *ri = p ? rin : rip;
+                ensure(q + 1);
+                const bool neg = q / nch == 1;
                 if (q + 2 < steps) emit_dma(q + 2, w);
-                for (uint32_t d = 0; d < 2; d++) {
-                    E.touch_addr(E.pos_bytes() + kTouchAhead + d * 8192u);
+                for (uint32_t d = 0; d < (d_notouch ? 0u : touch_count); d++) {
+                    E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
                     E.nop(4);
-                    E.code_touch();
+                    E.code_touch(kSinkV, kLane128V);
                 }
-                if (sec.nblk > 0) {
-                    if (!prefetched) emit_reads(sec, 0, q);
-                    E.wait_lgkm0();
-                }
-                for (int blk = 0; blk < sec.nblk; blk++) {
-                    if (blk + 1 < sec.nblk) emit_reads(sec, blk + 1, q);
-                    const int rhi = (blk + 1 < sec.nblk) ? sec.rows[(size_t)(blk + 1) * kBlockRows] : kJitChunk;
-                    // slot of a chunk row within this block
-                    int slot_of[kJitChunk];
-                    for (size_t i = (size_t)blk * kBlockRows; i < sec.rows.size() && sec.rows[i] < rhi; i++)
-                        slot_of[sec.rows[i]] = sec.slot[i];
-                    // columns in pairs, their entries interleaved (two independent
-                    // chains back to back); each column keeps ascending k
-                    for (int col = 0; col < kJitNW; col += 2) {
-                        int32_t &ia = cur[(size_t)col * 2 + p], &ib = cur[(size_t)(col + 1) * 2 + p];
-                        const int32_t ea = end[(size_t)col * 2 + p], eb = end[(size_t)(col + 1) * 2 + p];
-                        const uint32_t acca = kAcc0 + 2u * (uint32_t)col, accb = acca + 2u;
-                        for (;;) {
-                            const bool ha = ia < ea && ri[ia] < klo + rhi, hb = ib < eb && ri[ib] < klo + rhi;
-                            if (!ha && !hb) break;
-                            if (ha) E.pk_add(acca, kXSlot0 + 2u * (uint32_t)slot_of[ri[ia++] - klo], neg);
-                            if (hb) E.pk_add(accb, kXSlot0 + 2u * (uint32_t)slot_of[ri[ib++] - klo], neg);
+                const Section &sec = secs[q];
+                const int nrow = (int)sec.rows.size();
+                for (int i0 = 0; i0 < nrow; i0 += G) {
+                    const int i1 = std::min(nrow, i0 + G);
+                    const int64_t g0 = first[q] + i0, g1 = first[q] + i1;
+                    issue_reads(g1, q);  // (only if the schedule left the group unread)
+                    wait_rows(g1);
+                    issue_reads(g1 + RA, q + 1);
+                    if (row_major) {
+                        for (int i = i0; i < i1; i++) {
+                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % kJitSlots);
+                            for (uint8_t col : sec.cols[i]) E.pk_add(kAcc0 + 2u * col, x, neg);
                         }
+                    } else {
+                        // per column its entries of the group; columns in pairs, interleaved
+                        std::vector<std::vector<uint32_t>> xs(kJitNW);
+                        for (int i = i0; i < i1; i++) {
+                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % kJitSlots);
+                            for (uint8_t col : sec.cols[i]) xs[col].push_back(x);
+                        }
+                        for (int col = 0; col < kJitNW; col += 2)
+                            for (size_t k = 0; k < std::max(xs[col].size(), xs[col + 1].size()); k++) {
+                                if (k < xs[col].size()) E.pk_add(kAcc0 + 2u * col, xs[col][k], neg);
+                                if (k < xs[col + 1].size()) E.pk_add(kAcc0 + 2u * (col + 1), xs[col + 1][k], neg);
+                            }
                     }
-                    if (blk + 1 < sec.nblk) E.wait_lgkm0();
+                    (void)g0;
                 }
-                // next step's first block: its chunk is already resident (staged
-                // two steps ahead), so read it before the barrier
-                prefetched = false;
-                if (q + 1 < steps) {
-                    rows_of(q + 1, next);
-                    assign_slots(next);
-                    if (next.nblk > 0) {
-                        emit_reads(next, 0, q + 1);
-                        prefetched = true;
-                    }
-                }
+                issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first rows
                 E.wait_vm0();
-                E.barrier();
-                std::swap(sec, next);
+                if (!d_nobar) E.barrier();
             }
             E.restore_m0();
             E.ret();

@@ -11,26 +11,30 @@
 // indices at run time pays, per nonzero, for the index (LDS gather or
 // register-indexed add) and per column for a data-dependent branch -- the
 // measured cost of the register-X walk was 2-3x its adds.  Here every nonzero
-// of a wave's 64 columns is one v_pk_add_f32 (2 M rows per lane) whose X
+// of a wave's 32 columns is one v_pk_add_f32 (2 M rows per lane) whose X
 // register (a row of the current X^T block, loaded by ds_read_b64) and
 // accumulator are encoded in the instruction: no index traffic, no SALU, no
 // branch.  The same code serves every 128-row M tile.
 //
-// Workgroup: 128 M rows (2 per lane) x 8 waves x 64 columns, 512 threads, one
-// per CU (2 waves per SIMD).  The dispatcher sets up registers and calls the
+// Workgroup: 128 M rows (2 per lane) x W waves x NW columns, one per CU.
+// Geometry TSG_JIT_GEOM (as tsg_internal.h): 1 (default) 8 waves x 64
+// columns, 2 waves per SIMD, 256 VGPRs; 2: 16 waves x 32 columns, 4 waves per
+// SIMD, 128 VGPRs.  The dispatcher sets up registers and calls the
 // wave's generated stream ONCE; the stream itself runs the whole K loop:
 // X^T chunks of 96 rows in a ring of 3 LDS buffers, each staged by LDS-DMA two
 // steps ahead, one `s_waitcnt vmcnt(0); s_barrier` per step (step q = pass
 // p * nch + chunk j: p = 0 the +1 entries, p = 1 the -1 entries), the next
 // step's first X rows read before the barrier, the stream's own code touched
-// 8-24 KiB ahead (L2 prefetch).  Register contract (tsg_jit.cpp):
-//   v[8:103]    X slots (48 rows x 2 M rows)
-//   v104-v106   LDS byte address of lane row 0 in buffer 0/1/2
-//   v107        code-prefetch sink
-//   v108-v113   per-lane byte offsets (from the chunk base) of this wave's 6
-//               LDS-DMA pieces (2 rows each)
-//   v114        lane * 128 (code prefetch)
-//   v[116:243]  accumulators, column c of the wave at v[116+2c : 117+2c]
+// ahead (L2 prefetch).  Register contract (tsg_jit.cpp), S X slots, P DMA pieces:
+//   v[8 : 8+2S)   X slots (2 M rows each)
+//   next 3        LDS byte address of lane row 0 in buffer 0/1/2
+//   next 1        code-prefetch sink
+//   next P        per-lane byte offsets (from the chunk base) of this wave's
+//                 LDS-DMA pieces (2 rows each)
+//   next 1        lane * 128 (code prefetch)
+//   from the next even register: accumulators, column c at acc0 + 2c
+//   GEOM 1: S=48 -> v104-106, v107, v108-113, v114, acc v[116:243]
+//   GEOM 2: S=24 -> v56-58,   v59,  v60-62,   v63,  acc v[64:127]
 //   s[80:81] X^T base, s82 chunk stride in bytes, s[84:85] chunk base (stream),
 //   s86 saved M0, s[88:89] prefetch address (stream), s[92:93] region base,
 //   s[94:95] return address.
@@ -40,8 +44,11 @@
 
 namespace {
 
-constexpr int kJWaves = 8;
-constexpr int kJNW = 64;
+#ifndef TSG_JIT_GEOM
+#define TSG_JIT_GEOM 1
+#endif
+constexpr int kJWaves = TSG_JIT_GEOM == 1 ? 8 : 16;
+constexpr int kJNW = TSG_JIT_GEOM == 1 ? 64 : 32;
 constexpr int kJTileM = 128;
 constexpr int kJChunk = 96;
 constexpr int kJBufBytes = kJChunk * kJTileM * 4;  // 48 KiB
@@ -50,20 +57,29 @@ constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region head
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 
-#define TSG_JIT_CLOBBERS                                                                          \
+#if TSG_JIT_GEOM == 1
+#define TSG_JIT_CLOBBERS \
     "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", \
-        "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34",  \
-        "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47",  \
-        "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60",  \
-        "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73",  \
-        "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86",  \
-        "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99",  \
-        "v100", "v101", "v102", "v103", "v107", "s84", "s85", "s86", "s88", "s89", "s94", "s95",   \
+        "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", \
+        "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
+        "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", \
+        "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", \
+        "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", \
+        "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", \
+        "v100", "v101", "v102", "v103", "v107", "s84", "s85", "s86", "s88", "s89", "s94", "s95", \
         "scc", "memory"
+#else
+#define TSG_JIT_CLOBBERS \
+    "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", \
+        "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", \
+        "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
+        "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v59", "s84", "s85", "s86", "s88", \
+        "s89", "s94", "s95", "scc", "memory"
+#endif
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
+extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status)
@@ -91,19 +107,30 @@ extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
         return;
     }
 
-    // XCD-aware bijective remap: each XCD gets a contiguous n-tile-major run,
-    // so the M tiles of a column tile run together on one XCD and share its
-    // code through that XCD's L2.
+    // XCD-aware bijective remap: each XCD gets a contiguous run of workgroup
+    // ids (blocks b and b+8 share an XCD), and consecutive ids walk groups of
+    // kGN column tiles x kGM M tiles, so the ~32 workgroups an XCD runs at once
+    // share kGN code streams and kGM X^T slabs through its L2 instead of 1 and
+    // 32 (traffic beyond L2 = kGN x code + kGM x slab per round).
+#ifndef TSG_JIT_GN
+#define TSG_JIT_GN 4
+#endif
+#ifndef TSG_JIT_GM
+#define TSG_JIT_GM 8
+#endif
+    constexpr int kGN = TSG_JIT_GN, kGM = TSG_JIT_GM;
     const int T = mtiles * ntiles, L = blockIdx.x;
     const int xcd = L & 7, slot = L >> 3, q8 = T >> 3, r8 = T & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-    const int nt = wg / mtiles, mt = wg - nt * mtiles;
+    const int cb = wg / (kGN * mtiles), wc = min(kGN, ntiles - kGN * cb);  // column-tile block
+    const int loc = wg - cb * kGN * mtiles, g = loc / (wc * kGM), i = loc - g * wc * kGM;
+    const int nt = kGN * cb + i % wc, mt = kGM * g + i / wc;
     const int m0 = mt * kJTileM;
     const int ncol0 = nt * (kJWaves * kJNW) + wave * kJNW;
 
     const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + wave]);
     const uint32_t lb0 = (uint32_t)lane * 8u, lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
-    // LDS-DMA piece i of this wave: chunk rows 2*(wave*6 + i) + {0: lanes 0-31, 1: lanes 32-63}
+    // LDS-DMA piece i of this wave: chunk rows 2*(wave*P + i) + {0: lanes 0-31, 1: lanes 32-63}
     uint32_t off[kJPieces];
 #pragma unroll
     for (int i = 0; i < kJPieces; i++) {
@@ -113,6 +140,7 @@ extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
     const uint32_t l128 = (uint32_t)lane * 128u;
     const uint32_t stride = (uint32_t)kJChunk * (uint32_t)Mp * 4u;
 
+#if TSG_JIT_GEOM == 1
     F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
     asm volatile("s_getpc_b64 s[94:95]\n"
                  ".Ljr%=:\n\t"
@@ -125,6 +153,25 @@ extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
                    "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]), "{v110}"(off[2]),
                    "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
                  : TSG_JIT_CLOBBERS);
+    auto acc_of = [&](int c, int r) {
+        return c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
+             : c < 48 ? a2[2 * (c & 15) + r] : a3[2 * (c & 15) + r];
+    };
+#else
+    F32x32 a0 = {}, a1 = {};  // comp.h:41
+    asm volatile("s_getpc_b64 s[94:95]\n"
+                 ".Ljr%=:\n\t"
+                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
+                 "s_addc_u32 s95, s95, 0\n\t"
+                 "s_setpc_b64 %[cp]\n"
+                 ".Ljb%=:"
+                 : "+{v[64:95]}"(a0), "+{v[96:127]}"(a1)
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{v56}"(lb0),
+                   "{v57}"(lb1), "{v58}"(lb2), "{v60}"(off[0]), "{v61}"(off[1]), "{v62}"(off[2]),
+                   "{v63}"(l128)
+                 : TSG_JIT_CLOBBERS);
+    auto acc_of = [&](int c, int r) { return c < 16 ? a0[2 * (c & 15) + r] : a1[2 * (c & 15) + r]; };
+#endif
 
     if (ncol0 >= N) return;
 #pragma unroll
@@ -136,8 +183,7 @@ extern "C" __global__ __launch_bounds__(512, 1) void tsg_jit_kernel(
 #pragma unroll
         for (int c = 0; c < kJNW; c++) {
             const int n = ncol0 + c < N ? ncol0 + c : N - 1;
-            const float acc = c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
-                             : c < 48 ? a2[2 * (c & 15) + r] : a3[2 * (c & 15) + r];
+            const float acc = acc_of(c, r);
             float y = acc + b[n];                        // comp.h:63
             if (prelu) y = (y > 0) ? y : alpha[n] * y;   // comp_prelu.h:57-67
             v[c] = y;

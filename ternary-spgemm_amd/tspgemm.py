@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_info", "tcsc_hip_to_dense", "tcsc_hip_set_timing", "tcsc_hip_kernel_time",
     "tcsc_hip_last_error", "tcsc_hip_device_count", "tsg_tcsc_slice", "tsg_tcsc_validate",
     "tsg_gen_tcsc", "tsg_gen_x", "tcsc_hip_create_csc_packed", "tsg_tcsc_to_csc_packed",
-    "tsg_csc_packed_to_tcsc", "tsg_jit_codegen",
+    "tsg_csc_packed_to_tcsc", "tsg_jit_codegen", "tcsc_hip_kernel_name",
 )
 
 
@@ -93,6 +93,8 @@ def lib() -> C.CDLL:
     L.tcsc_hip_to_dense.argtypes = [H, vp, C.c_int, C.c_int]
     L.tcsc_hip_set_timing.argtypes = [H, C.c_int]
     L.tcsc_hip_kernel_time.argtypes = [H, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int]
+    L.tcsc_hip_kernel_name.argtypes = [H]
+    L.tcsc_hip_kernel_name.restype = C.c_char_p
     L.tcsc_hip_last_error.argtypes = []
     L.tcsc_hip_last_error.restype = C.c_char_p
     L.tcsc_hip_device_count.argtypes = [C.POINTER(C.c_int)]
@@ -109,7 +111,7 @@ def lib() -> C.CDLL:
     L.tsg_jit_codegen.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
                                   C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     for f in EXPORTED_SYMBOLS:
-        if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error"):
+        if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name"):
             getattr(L, f).restype = C.c_int
     _LIB = L
     return L
@@ -348,6 +350,10 @@ class TCSCDevice:
         o = tsg_info()
         _check(lib().tcsc_hip_info(self._h, C.byref(o)), "tcsc_hip_info")
         return {f: getattr(o, f) for f, _ in tsg_info._fields_}
+
+    def kernel_name(self) -> str:
+        """Device kernel this handle launches (default: the weight-compiled tsg_jit_kernel)."""
+        return lib().tcsc_hip_kernel_name(self._h).decode()
 
     def to_dense(self) -> np.ndarray:
         """getVectorRepresentation (DataStructureInterface.hpp:13)."""

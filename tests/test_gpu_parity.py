@@ -202,3 +202,27 @@ def test_csc_packed_input(tsg, oracle_mod):
         X = O.init_x_frac(M, K, s)
         b = np.linspace(-1, 1, N).astype(np.float32)
         assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+
+
+def test_default_is_weight_compiled(tsg, oracle_mod):
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(200, 70, 4, 3))
+    h = tsg.TCSCDevice(*t.arrays, 200, 70)
+    assert h.kernel_name() == "tsg_jit_kernel"
+
+
+@pytest.mark.parametrize("family,kernel", [("rx", "tsg_tcsc_rx_kernel"), ("stream", "tsg_tcsc_stream_kernel"),
+                                           ("flat", "tsg_tcsc_stream_kernel")])
+def test_other_kernel_families(tsg, oracle_mod, monkeypatch, family, kernel):
+    """The register-X and LDS-gather kernels (TSG_KERNEL at registration) stay
+    bit-exact too: they are the A/B baselines of DESIGN.md 9."""
+    monkeypatch.setenv("TSG_KERNEL", family)
+    O = oracle_mod
+    for M, K, N, s in [(129, 257, 65, 4), (300, 1000, 129, 16), (5, 1100, 300, 2)]:
+        t = O.tcsc_encode(O.gen_ternary(K, N, s, M + K))
+        h = tsg.TCSCDevice(*t.arrays, K, N)
+        assert h.kernel_name() == kernel
+        b = np.linspace(-1, 1, N).astype(np.float32)
+        X = O.init_x_frac(M, K, 3)
+        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+        h.close()

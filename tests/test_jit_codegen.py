@@ -2,7 +2,7 @@
 runs it.  tsg_jit_codegen's region is decoded instruction by instruction (only
 the gfx950 encodings the generator may emit are accepted) and a whole
 workgroup is emulated against the register contract of
-ternary-spgemm_amd/csrc/tsg_jit_kernel.hip: its 8 waves run barrier phase by
+ternary-spgemm_amd/csrc/tsg_jit_kernel.hip: its 16 waves run barrier phase by
 barrier phase, LDS-DMA copies land at the issuing wave's `s_waitcnt vmcnt(0)`,
 and every LDS read is checked to see data that landed in an EARLIER phase (no
 read-after-DMA race) while no DMA may overwrite rows read since it was issued
@@ -13,12 +13,27 @@ shows the GPU runs that code."""
 import numpy as np
 import pytest
 
-TILE_M, WAVES, NW, CHUNK, NBUF = 128, 8, 64, 96, 3
-TILE_COLS = WAVES * NW
-ROW_BYTES = TILE_M * 4
-BUF_BYTES = CHUNK * ROW_BYTES
-PIECES = CHUNK // WAVES // 2
+NBUF = 3
 MAGIC = (0x7453474A, 0x314A4954)
+
+
+class Geom:
+    """Geometry from the region header (words 2-3) and the register contract
+    of tsg_jit_kernel.hip derived from it."""
+
+    def __init__(self, code):
+        w2, w3 = int(code[2]), int(code[3])
+        self.waves, self.nw, self.chunk = w2 & 0xFF, (w2 >> 8) & 0xFF, w2 >> 16
+        self.slots, self.tile_m = w3 & 0xFFFF, w3 >> 16
+        self.tile_cols = self.waves * self.nw
+        self.row_bytes = self.tile_m * 4
+        self.buf_bytes = self.chunk * self.row_bytes
+        self.pieces = self.chunk // self.waves // 2
+        self.lds_v = 8 + 2 * self.slots
+        self.sink_v = self.lds_v + 3
+        self.dma_v = self.sink_v + 1
+        self.l128_v = self.dma_v + self.pieces
+        self.acc0 = (self.l128_v + 2) & ~1
 XT_BASE = 1 << 40  # fake device address of X^T
 
 
@@ -31,15 +46,18 @@ class Wave:
         self.base = None
         self.touch = None
         self.pending = []  # DMA copies not yet landed: (lds_byte, data, issue_phase)
+        self.reads = []    # X slot registers of LDS reads not yet waited for, oldest first
         self.done = False
 
 
-def _decode(code, pc):
+def _decode(code, pc, G):
     w0 = int(code[pc])
     w1 = int(code[pc + 1]) if pc + 1 < len(code) else None
     if (w0 & 0xFFFFFFF0) == 0xBF800000:
         return "nop", (), 1
-    simple = {0xBF8CC07F: "wait_lgkm", 0xBF8C0F70: "wait_vm", 0xBF8A0000: "barrier", 0xBED6007C: "save_m0",
+    if (w0 & 0xFFFFF0FF) == 0xBF8CC07F:
+        return "wait_lgkm", ((w0 >> 8) & 0xF,), 1
+    simple = {0xBF8C0F70: "wait_vm", 0xBF8A0000: "barrier", 0xBED6007C: "save_m0",
               0xBEFC0056: "restore_m0", 0xBED40150: "base_reset", 0xBE801D5E: "ret", 0x82558055: "base_addc",
               0x8259805D: "touch_addc", 0x80545254: "base_add"}
     if w0 in simple:
@@ -49,7 +67,7 @@ def _decode(code, pc):
     if w0 == 0x8058FF5C:
         return "touch_addr", (w1,), 2
     if w0 == 0xDC508000:
-        assert w1 == (107 << 24) | (88 << 16) | 114
+        assert w1 == (G.sink_v << 24) | (88 << 16) | G.l128_v
         return "touch", (), 2
     if w0 == 0xDDF48000:
         assert (w1 >> 16) == 84
@@ -59,7 +77,7 @@ def _decode(code, pc):
         src0, src1 = (w1 & 0x1FF) - 256, ((w1 >> 9) & 0x1FF) - 256
         assert (w1 >> 18) & 0x1FF == 0 and (w1 >> 27) & 3 == 3 and (w1 >> 29) == (2 if neg else 0)
         assert src0 == d, "v_pk_add_f32 must accumulate in place"
-        assert 116 <= d <= 242 and d % 2 == 0 and 8 <= src1 <= 102 and src1 % 2 == 0
+        assert G.acc0 <= d < G.acc0 + 2 * G.nw and d % 2 == 0 and 8 <= src1 < G.lds_v and src1 % 2 == 0
         return "add", (d, src1, neg), 2
     if (w0 & 0xFFFF0000) == 0xD8EC0000:  # ds_read_b64
         assert (w1 >> 8) & 0xFFFF == 0
@@ -68,7 +86,10 @@ def _decode(code, pc):
 
 
 def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
-    """One workgroup (column tile t, M tile at m0): returns acc[128 rows, 512 cols]."""
+    """One workgroup (column tile t, M tile at m0): returns acc[tile rows, tile cols]."""
+    G = Geom(code)
+    WAVES, NW, CHUNK, TILE_M, ROW_BYTES, BUF_BYTES, PIECES = (G.waves, G.nw, G.chunk, G.tile_m, G.row_bytes,
+                                                            G.buf_bytes, G.pieces)
     region_bytes = len(code) * 4
     stride = CHUNK * Mp * 4
     lanes = np.arange(64)
@@ -85,7 +106,7 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
             if wv.done:
                 continue
             while True:
-                kind, f, n = _decode(code, wv.pc)
+                kind, f, n = _decode(code, wv.pc, G)
                 wv.pc += n
                 if kind == "barrier":
                     at_barrier += 1
@@ -109,7 +130,7 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                 elif kind == "touch":
                     assert wv.touch is not None and wv.touch + 63 * 128 + 4 <= region_bytes, "prefetch past region"
                 elif kind == "glds":
-                    i = f[0] - 108
+                    i = f[0] - G.dma_v
                     assert 0 <= i < PIECES
                     chunk_row0 = 2 * (wv.w * PIECES + i)
                     j, rem = divmod(wv.base - XT_BASE, stride)
@@ -125,29 +146,38 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                         lds[dst // 4:dst // 4 + TILE_M] = data
                         landed[row] = phase
                     wv.pending = []
+                elif kind == "wait_lgkm":
+                    while len(wv.reads) > f[0]:  # LDS returns in order
+                        wv.reads.pop(0)
                 elif kind == "read":
                     vd, a, off = f
-                    assert 104 <= a <= 106 and off % ROW_BYTES == 0 and off // ROW_BYTES < CHUNK
-                    row = (a - 104) * CHUNK + off // ROW_BYTES
+                    assert vd not in wv.reads, "X slot reloaded before its previous read was waited for"
+                    wv.reads.append(vd)
+                    assert G.lds_v <= a < G.lds_v + 3 and off % ROW_BYTES == 0 and off // ROW_BYTES < CHUNK
+                    assert 8 <= vd < G.lds_v
+                    row = (a - G.lds_v) * CHUNK + off // ROW_BYTES
                     assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
                     last_read[row] = max(last_read[row], phase)
                     vals = lds[row * TILE_M:(row + 1) * TILE_M]
                     wv.v[vd:vd + 2] = vals.reshape(64, 2).T
                 elif kind == "add":
                     d, x, neg = f
+                    assert x not in wv.reads, "add reads an X slot whose LDS read may not have returned"
                     wv.v[d:d + 2] = wv.v[d:d + 2] - wv.v[x:x + 2] if neg else wv.v[d:d + 2] + wv.v[x:x + 2]
         assert at_barrier in (0, WAVES), "waves disagree on the barrier count"
         phase += 1
-    acc = np.zeros((TILE_M, TILE_COLS), np.float32)
+    acc = np.zeros((TILE_M, G.tile_cols), np.float32)
     for wv in waves:
         for c in range(NW):
             for r in range(2):
-                acc[r::2, wv.w * NW + c] = wv.v[116 + 2 * c + r]
+                acc[r::2, wv.w * NW + c] = wv.v[G.acc0 + 2 * c + r]
     return acc
 
 
 def emulate(code, wcode, X, K, N):
     assert tuple(int(x) for x in code[:2]) == MAGIC
+    G = Geom(code)
+    TILE_M, CHUNK, WAVES, TILE_COLS = G.tile_m, G.chunk, G.waves, G.tile_cols
     M = X.shape[0]
     nch = max(1, -(-K // CHUNK))
     Mp = -(-max(M, 1) // TILE_M) * TILE_M
