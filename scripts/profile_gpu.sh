@@ -1,6 +1,6 @@
 #!/bin/bash
 # Runs on the GPU box (via gpurun): kernel-trace stats + PMC passes of bench.py.
-# Usage: [PMC_SETS="A B;C D"] [NO_TRACE=1] scripts/profile_gpu.sh <tag> [bench args...]
+# Usage: [PMC_SETS="A B;C D"] [NO_TRACE=1] [NO_PMC=1] scripts/profile_gpu.sh <tag> [bench args...]
 # Each ';'-separated set is one rocprofv3 --pmc pass (kernel-trace only, never
 # combined with sys/runtime traces).
 set -u
@@ -12,8 +12,9 @@ DEFAULT="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_SALU SQ_WAVE
 IFS=';' read -ra SETS <<< "${PMC_SETS:-$DEFAULT}"
 if [ -z "${NO_TRACE:-}" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-      python3 bench.py --steps 5 --warmup 1 --cpu-rows 0 "$@" > $OUT/trace_bench.log 2>&1 || { echo "trace failed rc=$?"; exit 1; }
+      python3 bench.py --steps 20 --warmup 3 --cpu-rows 0 "$@" > $OUT/trace_bench.log 2>&1 || { echo "trace failed rc=$?"; exit 1; }
 fi
+[ -n "${NO_PMC:-}" ] && { echo profile done; exit 0; }
 i=0
 for CTR in "${SETS[@]}"; do
   i=$((i+1))
