@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""BASELINE configs[3]: M=4096 K=4096 N=16384, sparsity s in {2,4,8,16}, TCSC vs
+"CSC + packed values" (readme.md:111) as the registration format.  One GPU.
+
+Both formats register the same matrix (the packed one is converted on the host,
+tsg_csc_packed_to_tcsc) and run the same device kernel, so the comparison is
+format bytes and registration time; the kernel time per s is the sweep.  Every
+line also checks 8 sampled rows bit for bit against the CPU oracle.
+Writes one JSON object per s to stdout.
+
+    python scripts/sweep.py [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ternary-spgemm_amd"), os.path.join(REPO, "oracle")]
+import tspgemm as T  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--M", type=int, default=4096)
+    ap.add_argument("--K", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=16384)
+    a = ap.parse_args()
+    import torch
+    import oracle as O
+    dev = torch.device("cuda", 0)
+    M, K, N = a.M, a.K, a.N
+    g = torch.Generator(device=dev)
+    g.manual_seed(12345)
+    X = torch.randint(-512, 513, (M, K), generator=g, device=dev, dtype=torch.int32).to(torch.float32)
+    b = torch.full((N,), 2.0, device=dev)
+    Y = torch.empty((M, N), device=dev)
+    Xs = X[:8].cpu().numpy()
+    for s in (2, 4, 8, 16):
+        arrs = T.gen_tcsc(K, N, s, 42)
+        nnz = len(arrs[2]) + len(arrs[3])
+        col_ptr, row_idx, packed = T.tcsc_to_csc_packed(*arrs, N)
+        out = {"s": s, "M": M, "K": K, "N": N, "nnz": nnz,
+               "tcsc_bytes": 4 * (2 * (N + 1) + nnz),
+               "csc_packed_bytes": 4 * (N + 1) + 4 * len(row_idx) + len(packed)}
+        for fmt in ("tcsc", "csc_packed"):
+            t0 = time.time()
+            h = (T.TCSCDevice(*arrs, K, N, device=0) if fmt == "tcsc"
+                 else T.TCSCDevice.from_csc_packed(col_ptr, row_idx, packed, K, N, device=0))
+            out[f"{fmt}_register_s"] = round(time.time() - t0, 3)
+            h.reserve(M)
+            for _ in range(2):
+                h.gemm_torch(X, b, Y)
+            torch.cuda.synchronize()
+            h.set_timing(True)
+            h.kernel_time(reset=True)
+            for _ in range(a.steps):
+                h.gemm_torch(X, b, Y)
+            torch.cuda.synchronize()
+            ms, n = h.kernel_time(reset=True)
+            h.set_timing(False)
+            ms /= max(n, 1)
+            ref = O.base_tcsc(Xs, O.TCSC(*arrs, K, N), np.full(N, 2.0, np.float32))
+            out[f"{fmt}_kernel_ms"] = round(ms, 4)
+            out[f"{fmt}_bit_identical_rows"] = bool(np.array_equal(ref.view(np.uint32),
+                                                                   Y[:8].cpu().numpy().view(np.uint32)))
+            if fmt == "tcsc":
+                out["kernel"] = h.kernel_name()
+                out["gflops"] = round(T.flops(M, N, nnz) / (ms * 1e-3) / 1e9, 1)
+                out["valu_frac"] = round(T.flops(M, N, nnz) / (ms * 1e-3) / 78.64e12, 4)
+            h.close()
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
