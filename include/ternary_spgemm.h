@@ -52,6 +52,18 @@ int tcsc_hip_create(const int32_t *col_start_pos, const int32_t *col_start_neg,
  * TCSC.h:13-41; any value other than +1/-1 is treated as 0, as there). */
 int tcsc_hip_create_dense(const int32_t *W, int K, int N, int device, tsg_tcsc **out);
 
+/* GPU-side TCSC encoder (the TCSC ctor, TCSC.h:13-41, on the device): dW is a
+ * dense row-major K x N int32 ternary matrix in device memory; d_csp / d_csn
+ * (int32[N+1], caller-allocated device arrays) receive the column starts and
+ * *nnz_pos / *nnz_neg the entry counts (the call synchronises `stream` to
+ * return them).  When d_rip and d_rin are non-NULL (device arrays of at least
+ * rip_cap >= nnz_pos and rin_cap >= nnz_neg int32s) the row indices are filled
+ * too; call first with NULLs to size them.  Same arrays as tcsc_hip_create_dense
+ * builds on the host, bit for bit. */
+int tcsc_hip_encode_dense_dev(const int32_t *dW, int K, int N, int32_t *d_csp, int32_t *d_csn,
+                              int32_t *d_rip, int64_t rip_cap, int32_t *d_rin, int64_t rin_cap,
+                              int64_t *nnz_pos, int64_t *nnz_neg, void *stream);
+
 /* Same, from "CSC with compressed values vector (1s and -1s, 8 bits for 5
  * values)" (readme.md:111, the reference's optimisation idea 2): col_ptr
  * int32[N+1], row_idx int32[nnz] (ascending k per column), values base-3

@@ -351,11 +351,11 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
         }
         if (const char *d = std::getenv("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
             if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
-                for (size_t i = tsg::kJitWaves; i < h->jimg.wcode.size(); i++)
-                    h->jimg.wcode[i] = h->jimg.wcode[i % tsg::kJitWaves];
+                for (size_t i = tsg::kJitStreams; i < h->jimg.wcode.size(); i++)
+                    h->jimg.wcode[i] = h->jimg.wcode[i % tsg::kJitStreams];
             if (std::strstr(d, "samewave"))  // every wave of a tile runs its wave 0's stream
                 for (size_t i = 0; i < h->jimg.wcode.size(); i++)
-                    h->jimg.wcode[i] = h->jimg.wcode[i - i % tsg::kJitWaves];
+                    h->jimg.wcode[i] = h->jimg.wcode[i - i % tsg::kJitStreams];
             if (std::strstr(d, "pairwave"))  // waves 2i and 2i+1 share a stream
                 for (size_t i = 0; i < h->jimg.wcode.size(); i++) h->jimg.wcode[i] = h->jimg.wcode[i & ~(size_t)1];
         }
@@ -415,6 +415,36 @@ extern "C" int tcsc_hip_create_dense(const int32_t *W, int K, int N, int device,
     csp.push_back((int32_t)rip.size());
     csn.push_back((int32_t)rin.size());
     return tcsc_hip_create(csp.data(), csn.data(), rip.data(), rin.data(), K, N, device, out);
+}
+
+extern "C" int tcsc_hip_encode_dense_dev(const int32_t *dW, int K, int N, int32_t *d_csp, int32_t *d_csn,
+                                         int32_t *d_rip, int64_t rip_cap, int32_t *d_rin, int64_t rin_cap,
+                                         int64_t *nnz_pos, int64_t *nnz_neg, void *stream)
+{
+    if (K < 0 || N < 0 || !d_csp || !d_csn || !nnz_pos || !nnz_neg || (K > 0 && N > 0 && !dW))
+        return fail(TSG_ERR_ARG, "tcsc_hip_encode_dense_dev: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    size_t tmp_bytes = 0;
+    if (tsg::encode_count(dW, K, N, d_csp, d_csn, nullptr, &tmp_bytes, s) != 0)
+        return fail(TSG_ERR_HIP, "tcsc_hip_encode_dense_dev: scan workspace query failed");
+    void *tmp = nullptr;
+    HIP_TRY(hipMallocAsync(&tmp, std::max<size_t>(tmp_bytes, 4), s));
+    const int rc = tsg::encode_count(dW, K, N, d_csp, d_csn, tmp, &tmp_bytes, s);
+    HIP_TRY(hipFreeAsync(tmp, s));
+    if (rc != 0) return fail(TSG_ERR_HIP, std::string("tcsc_hip_encode_dense_dev: count/scan: ") +
+                                              hipGetErrorString(hipGetLastError()));
+    int32_t tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&tot[0], d_csp + N, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&tot[1], d_csn + N, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *nnz_pos = tot[0];
+    *nnz_neg = tot[1];
+    if (!d_rip || !d_rin) return TSG_OK;
+    if (rip_cap < tot[0] || rin_cap < tot[1])
+        return fail(TSG_ERR_ARG, "tcsc_hip_encode_dense_dev: row index arrays too small");
+    if (tsg::encode_fill(dW, K, N, d_csp, d_csn, d_rip, d_rin, s) != 0)
+        return fail(TSG_ERR_HIP, std::string("tcsc_hip_encode_dense_dev: fill: ") + hipGetErrorString(hipGetLastError()));
+    return TSG_OK;
 }
 
 extern "C" int tcsc_hip_create_csc_packed(const int32_t *col_ptr, const int32_t *row_idx,

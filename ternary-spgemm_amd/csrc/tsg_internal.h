@@ -115,26 +115,32 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 // ---------------------------------------------------------------------------
 // "jit" (weight-compiled) kernel: dispatcher tsg_jit_kernel (tsg_jit_kernel.hip,
 // built as the code object lib/tsg_jit.co) + machine code generated from the
-// TCSC arrays (tsg_jit.cpp).  Workgroup: 128 M rows (2 per lane) x W waves x
-// NW columns; X^T chunks of 96 K rows in a ring of 3 LDS buffers (144 KiB).
-// Geometry (compile time, TSG_JIT_GEOM, shared with tsg_jit_kernel.hip):
-//   1 (default): 8 waves x 64 columns, 48 X slots, 2 waves per SIMD
-//   2:          16 waves x 32 columns, 24 X slots, 4 waves per SIMD
+// TCSC arrays (tsg_jit.cpp).  A workgroup covers kJitTileM M rows (2 per lane)
+// x kJitTileCols columns; each generated stream owns kJitNW columns and is run
+// by kJitMSplit waves (one per 128-row M slice); X^T chunks of kJitChunk K rows
+// in a ring of 3 LDS buffers (144 KiB).  Geometry (compile time, TSG_JIT_GEOM,
+// shared with tsg_jit_kernel.hip):
+//   1 (default): 8 waves x 64 columns x 128 M rows, 48 X slots, 2 waves/SIMD
+//   2:          16 waves x 32 columns x 128 M rows, 24 X slots, 4 waves/SIMD
+//   3:           8 waves = 4 streams x 2 M slices, 64 columns, 256 M rows:
+//                pairs of waves share a stream (instruction fetch)
 #ifndef TSG_JIT_GEOM
 #define TSG_JIT_GEOM 1
 #endif
-constexpr int kJitTileM = 128;
-constexpr int kJitWaves = TSG_JIT_GEOM == 1 ? 8 : 16;
-constexpr int kJitNW = TSG_JIT_GEOM == 1 ? 64 : 32;
-constexpr int kJitTileCols = kJitWaves * kJitNW;
-constexpr int kJitChunk = 96;
-constexpr int kJitSlots = TSG_JIT_GEOM == 1 ? 48 : 24;  // X slot registers v[8 : 8 + 2 * slots)
+constexpr int kJitTileM = TSG_JIT_GEOM == 3 ? 256 : 128;
+constexpr int kJitWaves = TSG_JIT_GEOM == 2 ? 16 : 8;
+constexpr int kJitMSplit = TSG_JIT_GEOM == 3 ? 2 : 1;
+constexpr int kJitStreams = kJitWaves / kJitMSplit;     // streams per column tile
+constexpr int kJitNW = TSG_JIT_GEOM == 2 ? 32 : 64;
+constexpr int kJitTileCols = kJitStreams * kJitNW;
+constexpr int kJitChunk = TSG_JIT_GEOM == 3 ? 48 : 96;
+constexpr int kJitSlots = TSG_JIT_GEOM == 2 ? 24 : 48;  // X slot registers v[8 : 8 + 2 * slots)
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
 
 struct JitImage {
     int K = 0, N = 0, Npad = 0, nch = 0;
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
-    std::vector<uint32_t> wcode;   // per (column tile, wave): byte offset of its stream
+    std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
 };
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                     const int32_t *rin, int K, int N, JitImage &img);
@@ -167,6 +173,14 @@ int pick_tile_cols(int N);
 
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                           const int32_t *rin, int K, int N);
+
+// GPU-side TCSC encoder (csrc/tsg_encode.hip).  encode_count: column starts
+// into d_csp/d_csn (N+1 each); with d_tmp == nullptr it only returns the scan
+// workspace size in *tmp_bytes.  encode_fill: row indices.
+int encode_count(const int32_t *dW, int K, int N, int32_t *d_csp, int32_t *d_csn, void *d_tmp, size_t *tmp_bytes,
+                 void *stream);
+int encode_fill(const int32_t *dW, int K, int N, const int32_t *d_csp, const int32_t *d_csn, int32_t *d_rip,
+                int32_t *d_rin, void *stream);
 
 // Kernel launchers (csrc/tcsc_kernels.hip).  All enqueue on `stream`.
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream);

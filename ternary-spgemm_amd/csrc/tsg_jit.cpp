@@ -66,7 +66,7 @@ struct Emit {
         c.push_back(0xdc508000u);
         c.push_back((sink << 24) | (88u << 16) | l128);
     }
-    void m0_lit(uint32_t v) { align8(); c.push_back(0xbefc00ffu); c.push_back(v); }  // s_mov_b32 m0, v
+    void m0_wave(uint32_t v) { align8(); c.push_back(0x807cff53u); c.push_back(v); }  // s_add_u32 m0, s83, v
     void save_m0() { c.push_back(0xbed6007cu); }      // s_mov_b32 s86, m0
     void restore_m0() { c.push_back(0xbefc0056u); }   // s_mov_b32 m0, s86
     void base_reset() { c.push_back(0xbed40150u); }   // s_mov_b64 s[84:85], s[80:81]
@@ -93,18 +93,19 @@ struct Emit {
 // Register contract (tsg_jit_kernel.hip): X slots v[8 : 8 + 2S), then 3 LDS
 // buffer bases, the code-prefetch sink, the DMA piece offsets, lane*128, and
 // the accumulators from the next even register.
-constexpr int kPieces = kJitChunk / kJitWaves / 2;        // DMA pieces per wave per chunk
+constexpr uint32_t kRowBytes = kJitTileM * 4;             // one X^T row of the tile in LDS
+constexpr uint32_t kBufBytes = kJitChunk * kRowBytes;     // one LDS chunk buffer
+constexpr int kPieceRows = 1024 / kRowBytes;              // rows per 1-KiB LDS-DMA piece
+constexpr int kPieces = kJitChunk / kPieceRows / kJitWaves;  // DMA pieces per wave per chunk
+static_assert(kPieces * kPieceRows * kJitWaves == kJitChunk, "chunk rows split in pieces over the waves");
 constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 2s : 9 + 2s]
 constexpr uint32_t kLdsBaseV = kXSlot0 + 2 * kJitSlots;   // + b: lane row 0 of LDS buffer b
 constexpr uint32_t kSinkV = kLdsBaseV + 3;
 constexpr uint32_t kDmaOffV = kSinkV + 1;                  // + i: DMA piece i offsets
 constexpr uint32_t kLane128V = kDmaOffV + kPieces;
 constexpr uint32_t kAcc0 = (kLane128V + 2) & ~1u;         // column c: v[acc0 + 2c : acc0 + 2c + 1]
-static_assert(kAcc0 + 2 * kJitNW <= (TSG_JIT_GEOM == 1 ? 256u : 128u), "VGPR budget");
-constexpr uint32_t kRowBytes = kJitTileM * 4;             // one X^T row of the tile in LDS
-constexpr uint32_t kBufBytes = kJitChunk * kRowBytes;     // one LDS chunk buffer
+static_assert(kAcc0 + 2 * kJitNW <= (TSG_JIT_GEOM == 2 ? 128u : 256u), "VGPR budget");
 constexpr int kTailPad = 32768 + 1024;   // words of padding after the last stream (code prefetch reads ahead)
-static_assert(kJitChunk % (2 * kJitWaves) == 0, "chunk rows split in 2-row pieces over the waves");
 static_assert((kJitChunk - 1) * kRowBytes < 65536, "ds_read offset field");
 
 // One step's work for a wave: the chunk rows its columns use, ascending, and
@@ -124,16 +125,17 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     img.Npad = ((N + kJitTileCols - 1) / kJitTileCols) * kJitTileCols;
     img.nch = std::max(1, (K + kJitChunk - 1) / kJitChunk);
     const int nch = img.nch, ntiles = img.Npad / kJitTileCols, steps = 2 * nch;
-    img.wcode.assign((size_t)ntiles * kJitWaves, 0u);
+    img.wcode.assign((size_t)ntiles * kJitStreams, 0u);
     std::vector<uint32_t> &code = img.code;
     code.clear();
     const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
-    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitWaves * (steps * 220 + 64) + kTailPad + 64);
+    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitStreams * (steps * 220 + 64) + kTailPad + 64);
     // header: magic, then the geometry (tests/test_jit_codegen.py derives the
     // register contract from it)
     code.insert(code.end(), {kJitMagic0, kJitMagic1,
                              (uint32_t)kJitWaves | (uint32_t)kJitNW << 8 | (uint32_t)kJitChunk << 16,
-                             (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16});
+                             (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
+                             (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, 0u, 0u, 0u});
     Emit E{code};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
@@ -166,7 +168,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             }
     };
     int base_chunk = -1;  // chunk whose base s[84:85] holds
-    auto emit_dma = [&](int q, int w) {  // stage step q's chunk into LDS buffer q % 3
+    // stage step q's chunk into LDS buffer q % 3; M0 = s83 (this wave's first
+    // piece, set by the dispatcher) + buffer + piece offset
+    auto emit_dma = [&](int q) {
         if (d_nodma) return;
         const int j = q % nch;
         if (j == 0) {
@@ -182,7 +186,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         base_chunk = j;
         E.nop(4);  // SALU-written SGPR base -> VMEM
         for (int i = 0; i < kPieces; i++) {
-            E.m0_lit((uint32_t)(q % 3) * kBufBytes + (uint32_t)(2 * (w * kPieces + i)) * kRowBytes);
+            E.m0_wave((uint32_t)(q % 3) * kBufBytes + (uint32_t)i * 1024u);
             E.nop(0);  // M0 -> LDS-DMA
             E.glds_x4(kDmaOffV + (uint32_t)i);
         }
@@ -205,9 +209,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         RA = kJitSlots / 2;
     }
     for (int t = 0; t < ntiles; t++) {
-        for (int w = 0; w < kJitWaves; w++) {
+        for (int w = 0; w < kJitStreams; w++) {
             while (code.size() % 64) E.nop();  // 256-B aligned stream start
-            img.wcode[(size_t)t * kJitWaves + w] = E.pos_bytes();
+            img.wcode[(size_t)t * kJitStreams + w] = E.pos_bytes();
             const int n0 = t * kJitTileCols + w * kJitNW;
             for (int col = 0; col < kJitNW; col++)
                 for (int p = 0; p < 2; p++) {
@@ -219,8 +223,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             base_chunk = -1;
             E.save_m0();
             // prologue: steps 0 and 1 staged, landed, visible
-            emit_dma(0, w);
-            emit_dma(1, w);
+            emit_dma(0);
+            emit_dma(1);
             E.wait_vm0();
             E.barrier();
             std::vector<Section> secs(steps);
@@ -256,7 +260,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             for (int q = 0; q < steps; q++) {
                 ensure(q + 1);
                 const bool neg = q / nch == 1;
-                if (q + 2 < steps) emit_dma(q + 2, w);
+                if (q + 2 < steps) emit_dma(q + 2);
                 for (uint32_t d = 0; d < (d_notouch ? 0u : touch_count); d++) {
                     E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
                     E.nop(4);

@@ -16,10 +16,13 @@
 // accumulator are encoded in the instruction: no index traffic, no SALU, no
 // branch.  The same code serves every 128-row M tile.
 //
-// Workgroup: 128 M rows (2 per lane) x W waves x NW columns, one per CU.
+// Workgroup: kJTileM M rows x kJTileCols columns, one per CU; a wave owns 2
+// rows per lane of one 128-row M slice and the kJNW columns of its stream.
 // Geometry TSG_JIT_GEOM (as tsg_internal.h): 1 (default) 8 waves x 64
 // columns, 2 waves per SIMD, 256 VGPRs; 2: 16 waves x 32 columns, 4 waves per
-// SIMD, 128 VGPRs.  The dispatcher sets up registers and calls the
+// SIMD, 128 VGPRs; 3: 8 waves = 4 streams x 2 M slices (a stream's code is
+// fetched once for 2 waves), 64 columns, 256 M rows.  The dispatcher sets up
+// registers and calls the
 // wave's generated stream ONCE; the stream itself runs the whole K loop:
 // X^T chunks of 96 rows in a ring of 3 LDS buffers, each staged by LDS-DMA two
 // steps ahead, one `s_waitcnt vmcnt(0); s_barrier` per step (step q = pass
@@ -35,7 +38,8 @@
 //   from the next even register: accumulators, column c at acc0 + 2c
 //   GEOM 1: S=48 -> v104-106, v107, v108-113, v114, acc v[116:243]
 //   GEOM 2: S=24 -> v56-58,   v59,  v60-62,   v63,  acc v[64:127]
-//   s[80:81] X^T base, s82 chunk stride in bytes, s[84:85] chunk base (stream),
+//   s[80:81] X^T base, s82 chunk stride in bytes, s83 LDS byte offset of this
+//   wave's first DMA piece, s[84:85] chunk base (stream),
 //   s86 saved M0, s[88:89] prefetch address (stream), s[92:93] region base,
 //   s[94:95] return address.
 #include <hip/hip_runtime.h>
@@ -47,17 +51,21 @@ namespace {
 #ifndef TSG_JIT_GEOM
 #define TSG_JIT_GEOM 1
 #endif
-constexpr int kJWaves = TSG_JIT_GEOM == 1 ? 8 : 16;
-constexpr int kJNW = TSG_JIT_GEOM == 1 ? 64 : 32;
-constexpr int kJTileM = 128;
-constexpr int kJChunk = 96;
-constexpr int kJBufBytes = kJChunk * kJTileM * 4;  // 48 KiB
-constexpr int kJPieces = kJChunk / kJWaves / 2;     // LDS-DMA pieces per wave per chunk
+constexpr int kJWaves = TSG_JIT_GEOM == 2 ? 16 : 8;
+constexpr int kJMSplit = TSG_JIT_GEOM == 3 ? 2 : 1;
+constexpr int kJStreams = kJWaves / kJMSplit;
+constexpr int kJNW = TSG_JIT_GEOM == 2 ? 32 : 64;
+constexpr int kJTileM = TSG_JIT_GEOM == 3 ? 256 : 128;
+constexpr int kJTileCols = kJStreams * kJNW;
+constexpr int kJChunk = TSG_JIT_GEOM == 3 ? 48 : 96;
+constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB
+constexpr int kJPieceRows = 1024 / (kJTileM * 4);    // X^T rows per 1-KiB LDS-DMA piece
+constexpr int kJPieces = kJChunk / kJPieceRows / kJWaves;  // LDS-DMA pieces per wave per chunk
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 
-#if TSG_JIT_GEOM == 1
+#if TSG_JIT_GEOM != 2
 #define TSG_JIT_CLOBBERS \
     "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", \
         "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", \
@@ -126,21 +134,24 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const int loc = wg - cb * kGN * mtiles, g = loc / (wc * kGM), i = loc - g * wc * kGM;
     const int nt = kGN * cb + i % wc, mt = kGM * g + i / wc;
     const int m0 = mt * kJTileM;
-    const int ncol0 = nt * (kJWaves * kJNW) + wave * kJNW;
+    const int stream = wave % kJStreams, ms = wave / kJStreams;  // column stream, 128-row M slice
+    const int ncol0 = nt * kJTileCols + stream * kJNW;
 
-    const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + wave]);
-    const uint32_t lb0 = (uint32_t)lane * 8u, lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
-    // LDS-DMA piece i of this wave: chunk rows 2*(wave*P + i) + {0: lanes 0-31, 1: lanes 32-63}
+    const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJStreams + stream]);
+    const uint32_t lb0 = (uint32_t)(ms * 512 + lane * 8), lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
+    // LDS-DMA piece i of this wave: chunk rows kJPieceRows*(wave*P + i) + lane / (64 / kJPieceRows)
+    constexpr int kLanesPerRow = 64 / kJPieceRows;
     uint32_t off[kJPieces];
 #pragma unroll
     for (int i = 0; i < kJPieces; i++) {
-        const uint32_t r = 2u * (uint32_t)(wave * kJPieces + i) + (uint32_t)(lane >> 5);
-        off[i] = (r * (uint32_t)Mp + (uint32_t)m0 + 4u * (uint32_t)(lane & 31)) * 4u;
+        const uint32_t r = (uint32_t)(kJPieceRows * (wave * kJPieces + i) + lane / kLanesPerRow);
+        off[i] = (r * (uint32_t)Mp + (uint32_t)m0 + 4u * (uint32_t)(lane % kLanesPerRow)) * 4u;
     }
+    const uint32_t wb = (uint32_t)(wave * kJPieces) * 1024u;  // s83
     const uint32_t l128 = (uint32_t)lane * 128u;
     const uint32_t stride = (uint32_t)kJChunk * (uint32_t)Mp * 4u;
 
-#if TSG_JIT_GEOM == 1
+#if TSG_JIT_GEOM != 2
     F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
     asm volatile("s_getpc_b64 s[94:95]\n"
                  ".Ljr%=:\n\t"
@@ -149,9 +160,9 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  "s_setpc_b64 %[cp]\n"
                  ".Ljb%=:"
                  : "+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3)
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{v104}"(lb0),
-                   "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]), "{v110}"(off[2]),
-                   "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
+                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
+                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
                  : TSG_JIT_CLOBBERS);
     auto acc_of = [&](int c, int r) {
         return c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
@@ -166,7 +177,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  "s_setpc_b64 %[cp]\n"
                  ".Ljb%=:"
                  : "+{v[64:95]}"(a0), "+{v[96:127]}"(a1)
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{v56}"(lb0),
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
+                   "{v56}"(lb0),
                    "{v57}"(lb1), "{v58}"(lb2), "{v60}"(off[0]), "{v61}"(off[1]), "{v62}"(off[2]),
                    "{v63}"(l128)
                  : TSG_JIT_CLOBBERS);
@@ -176,7 +188,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     if (ncol0 >= N) return;
 #pragma unroll
     for (int r = 0; r < 2; r++) {
-        const int m = m0 + 2 * lane + r;
+        const int m = m0 + ms * 128 + 2 * lane + r;
         if (m >= M) continue;
         float *yrow = Y + (size_t)m * N + ncol0;
         float v[kJNW];

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_info", "tcsc_hip_to_dense", "tcsc_hip_set_timing", "tcsc_hip_kernel_time",
     "tcsc_hip_last_error", "tcsc_hip_device_count", "tsg_tcsc_slice", "tsg_tcsc_validate",
     "tsg_gen_tcsc", "tsg_gen_x", "tcsc_hip_create_csc_packed", "tsg_tcsc_to_csc_packed",
-    "tsg_csc_packed_to_tcsc", "tsg_jit_codegen", "tcsc_hip_kernel_name",
+    "tsg_csc_packed_to_tcsc", "tsg_jit_codegen", "tcsc_hip_kernel_name", "tcsc_hip_encode_dense_dev",
 )
 
 
@@ -93,6 +93,8 @@ def lib() -> C.CDLL:
     L.tcsc_hip_to_dense.argtypes = [H, vp, C.c_int, C.c_int]
     L.tcsc_hip_set_timing.argtypes = [H, C.c_int]
     L.tcsc_hip_kernel_time.argtypes = [H, C.POINTER(C.c_double), C.POINTER(C.c_int64), C.c_int]
+    L.tcsc_hip_encode_dense_dev.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp, C.c_int64,
+                                            C.POINTER(C.c_int64), C.POINTER(C.c_int64), vp]
     L.tcsc_hip_kernel_name.argtypes = [H]
     L.tcsc_hip_kernel_name.restype = C.c_char_p
     L.tcsc_hip_last_error.argtypes = []
@@ -221,6 +223,29 @@ def jit_codegen(csp, csn, rip, rin, K: int, N: int):
     return code, wcode
 
 
+def encode_dense_torch(W):
+    """GPU-side TCSC encoder (TCSC.h:13-41 on the device): W is a [K, N] int32
+    CUDA tensor; returns (csp, csn, rip, rin) as int32 CUDA tensors on W's device,
+    on the current stream (tcsc_hip_encode_dense_dev)."""
+    import torch
+    assert W.is_cuda and W.dtype == torch.int32 and W.dim() == 2 and W.is_contiguous()
+    K, N = W.shape
+    dev = W.device
+    csp = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    csn = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    p, q = C.c_int64(), C.c_int64()
+    s = torch.cuda.current_stream(dev).cuda_stream
+    L = lib()
+    _check(L.tcsc_hip_encode_dense_dev(W.data_ptr(), K, N, csp.data_ptr(), csn.data_ptr(), None, 0, None, 0,
+                                       C.byref(p), C.byref(q), s), "tcsc_hip_encode_dense_dev")
+    rip = torch.empty(max(p.value, 1), dtype=torch.int32, device=dev)
+    rin = torch.empty(max(q.value, 1), dtype=torch.int32, device=dev)
+    _check(L.tcsc_hip_encode_dense_dev(W.data_ptr(), K, N, csp.data_ptr(), csn.data_ptr(), rip.data_ptr(),
+                                       rip.numel(), rin.data_ptr(), rin.numel(), C.byref(p), C.byref(q), s),
+           "tcsc_hip_encode_dense_dev")
+    return csp, csn, rip[: p.value], rin[: q.value]
+
+
 def gen_x(M: int, K: int, seed: int, rng: int = 512) -> np.ndarray:
     """Integer-valued fp32 X in [-rng, rng] (initX, sparseUtils.h:6-23)."""
     X = np.empty((M, K), np.float32)
@@ -272,6 +297,15 @@ class TCSCDevice:
                "tcsc_hip_create_dense")
         self._h = h
         return self
+
+    @classmethod
+    def from_dense_torch(cls, W, device: int = -1) -> "TCSCDevice":
+        """Registration from a dense [K, N] int32 CUDA tensor: the TCSC is built on
+        the GPU (encode_dense_torch, TCSC.h:13-41) and compiled from its arrays."""
+        csp, csn, rip, rin = encode_dense_torch(W)
+        K, N = W.shape
+        return cls(csp.cpu().numpy(), csn.cpu().numpy(), rip.cpu().numpy(), rin.cpu().numpy(), K, N,
+                   device=W.device.index if device < 0 else device)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

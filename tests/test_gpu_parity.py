@@ -226,3 +226,28 @@ def test_other_kernel_families(tsg, oracle_mod, monkeypatch, family, kernel):
         X = O.init_x_frac(M, K, 3)
         assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
         h.close()
+
+
+def test_gpu_encoder_matches_host_ctor(tsg, oracle_mod):
+    """GPU-side TCSC encoder == the TCSC ctor (TCSC.h:13-41)
+    array for array, incl. the 4x4 KAT, values other than +-1 (zeros there),
+    empty columns and a registration through it."""
+    import torch
+    O = oracle_mod
+    kat = json.load(open(os.path.join(GOLDEN, "kat_tcsc_4x4.json")))
+    cases = [np.array(kat["W"], np.int32), O.gen_ternary(300, 70, 4, 1), O.gen_ternary(1000, 513, 2, 2),
+             O.gen_ternary(129, 1, 16, 3), np.zeros((5, 7), np.int32)]
+    odd = O.gen_ternary(64, 33, 4, 4)
+    odd[::7, ::3] = 2
+    odd[3::11, 1::5] = -5
+    cases.append(odd)
+    for W in cases:
+        t = O.tcsc_encode(np.where(np.abs(W) == 1, W, 0).astype(np.int32))
+        g = tsg.encode_dense_torch(torch.from_numpy(np.ascontiguousarray(W)).cuda())
+        for a, b in zip(t.arrays, g):
+            assert np.array_equal(np.asarray(a, np.int32), b.cpu().numpy())
+    W = O.gen_ternary(700, 300, 4, 9)
+    h = tsg.TCSCDevice.from_dense_torch(torch.from_numpy(W).cuda())
+    X = O.init_x_frac(77, 700, 1)
+    b = np.linspace(-1, 1, 300).astype(np.float32)
+    assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, O.tcsc_encode(W), b))

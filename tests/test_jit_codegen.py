@@ -22,13 +22,16 @@ class Geom:
     of tsg_jit_kernel.hip derived from it."""
 
     def __init__(self, code):
-        w2, w3 = int(code[2]), int(code[3])
+        w2, w3, w4 = int(code[2]), int(code[3]), int(code[4])
         self.waves, self.nw, self.chunk = w2 & 0xFF, (w2 >> 8) & 0xFF, w2 >> 16
         self.slots, self.tile_m = w3 & 0xFFFF, w3 >> 16
-        self.tile_cols = self.waves * self.nw
+        self.streams, self.msplit = w4 & 0xFF, (w4 >> 8) & 0xFF
+        assert self.streams * self.msplit == self.waves and self.tile_m == 128 * self.msplit
+        self.tile_cols = self.streams * self.nw
         self.row_bytes = self.tile_m * 4
         self.buf_bytes = self.chunk * self.row_bytes
-        self.pieces = self.chunk // self.waves // 2
+        self.piece_rows = 1024 // self.row_bytes
+        self.pieces = self.chunk // self.piece_rows // self.waves
         self.lds_v = 8 + 2 * self.slots
         self.sink_v = self.lds_v + 3
         self.dma_v = self.sink_v + 1
@@ -62,7 +65,7 @@ def _decode(code, pc, G):
               0x8259805D: "touch_addc", 0x80545254: "base_add"}
     if w0 in simple:
         return simple[w0], (), 1
-    if w0 == 0xBEFC00FF:
+    if w0 == 0x807CFF53:  # s_add_u32 m0, s83, lit
         return "m0", (w1,), 2
     if w0 == 0x8058FF5C:
         return "touch_addr", (w1,), 2
@@ -96,9 +99,10 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
     lds = np.zeros(NBUF * BUF_BYTES // 4, np.float32)
     landed = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)   # phase a row's data landed
     last_read = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)
-    waves = [Wave(w, int(wcode[t * WAVES + w]) // 4) for w in range(WAVES)]
+    S = G.streams
+    waves = [Wave(w, int(wcode[t * S + w % S]) // 4) for w in range(WAVES)]
     for wv in waves:
-        assert int(wcode[t * WAVES + wv.w]) % 256 == 0
+        assert int(wcode[t * S + wv.w % S]) % 256 == 0
     phase = 0
     while not all(wv.done for wv in waves):
         at_barrier = 0
@@ -120,7 +124,7 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                 elif kind == "restore_m0":
                     wv.m0 = wv.saved_m0
                 elif kind == "m0":
-                    wv.m0 = f[0]
+                    wv.m0 = wv.w * PIECES * 1024 + f[0]  # s83 = the wave's first DMA piece
                 elif kind == "base_reset":
                     wv.base = XT_BASE
                 elif kind == "base_add":
@@ -132,11 +136,11 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                 elif kind == "glds":
                     i = f[0] - G.dma_v
                     assert 0 <= i < PIECES
-                    chunk_row0 = 2 * (wv.w * PIECES + i)
+                    chunk_row0 = G.piece_rows * (wv.w * PIECES + i)
                     j, rem = divmod(wv.base - XT_BASE, stride)
                     assert rem == 0 and 0 <= j < nch
                     assert wv.m0 % BUF_BYTES == chunk_row0 * ROW_BYTES, "DMA lands on the wrong rows"
-                    for half in range(2):
+                    for half in range(G.piece_rows):
                         src = XT[j * CHUNK + chunk_row0 + half, m0:m0 + TILE_M]
                         wv.pending.append((wv.m0 + half * ROW_BYTES, src.copy(), phase))
                 elif kind == "wait_vm":
@@ -158,7 +162,8 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                     row = (a - G.lds_v) * CHUNK + off // ROW_BYTES
                     assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
                     last_read[row] = max(last_read[row], phase)
-                    vals = lds[row * TILE_M:(row + 1) * TILE_M]
+                    ms = wv.w // S  # the wave's 128-row M slice of the 256- or 128-row tile
+                    vals = lds[row * TILE_M + ms * 128:row * TILE_M + ms * 128 + 128]
                     wv.v[vd:vd + 2] = vals.reshape(64, 2).T
                 elif kind == "add":
                     d, x, neg = f
@@ -168,9 +173,10 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
         phase += 1
     acc = np.zeros((TILE_M, G.tile_cols), np.float32)
     for wv in waves:
+        ms, st = wv.w // S, wv.w % S
         for c in range(NW):
             for r in range(2):
-                acc[r::2, wv.w * NW + c] = wv.v[G.acc0 + 2 * c + r]
+                acc[ms * 128 + r:ms * 128 + 128:2, st * NW + c] = wv.v[G.acc0 + 2 * c + r]
     return acc
 
 
@@ -183,7 +189,7 @@ def emulate(code, wcode, X, K, N):
     Mp = -(-max(M, 1) // TILE_M) * TILE_M
     XT = np.zeros((nch * CHUNK, Mp), np.float32)
     XT[:K, :M] = X.T
-    ntiles = len(wcode) // WAVES
+    ntiles = len(wcode) // G.streams
     Y = np.zeros((Mp, ntiles * TILE_COLS), np.float32)
     for t in range(ntiles):
         for m0 in range(0, Mp, TILE_M):
