@@ -7,6 +7,10 @@
 //   auto sf_csc = std::make_shared<TCSC>(W_raw.data(), K, N);     // cpp_impl/main.cpp:63
 //   add_function(tsg::make_hip_comp_func(*sf_csc, K, N), "HipBaseTCSC");
 //
+//   auto sf_blocked = std::make_shared<BlockedTCSC<BLOCK_SIZE>>(W_raw.data(), K, N);  // main.cpp:69
+//   add_function(tsg::make_hip_comp_func(*sf_blocked, K, N), "HipBaseBlockedTCSC");
+//   (BaseBlockedTCSC, comp.h:607-658; B deduced from BlockedTCSC<B>)
+//
 // HipTCSC also implements DataStructureInterface (init / getVectorRepresentation,
 // cpp_impl/data_structures/DataStructureInterface.hpp:10-13); define
 // TSG_WITH_REFERENCE_DSI after including the reference's header to inherit it.
@@ -58,6 +62,19 @@ public:
         check(tcsc_hip_create(t.col_start_pos.data(), t.col_start_neg.data(),
                               t.row_index_pos.data(), t.row_index_neg.data(), K, N, device, &h),
               "tcsc_hip_create");
+        h_.reset(h, tcsc_hip_destroy);
+    }
+
+    // From a BlockedTCSC<B>-shaped object (data_structures/BlockedTCSC.h:7-13):
+    // calls compute BaseBlockedTCSC<float, B> (tcsc_hip_create_blocked).
+    struct Blocked {};
+    template <class BlockedLike>
+    HipTCSC(Blocked, const BlockedLike &t, int K, int N, int B, int device = -1) : K_(K), N_(N), device_(device)
+    {
+        tsg_tcsc *h = nullptr;
+        check(tcsc_hip_create_blocked(t.col_start_pos.data(), t.col_start_neg.data(), t.row_index_pos.data(),
+                                      t.row_index_neg.data(), K, N, B, device, &h),
+              "tcsc_hip_create_blocked");
         h_.reset(h, tcsc_hip_destroy);
     }
 
@@ -115,6 +132,14 @@ template <class TCSCLike>
 comp_func make_hip_comp_func(const TCSCLike &t, int K, int N, int device = -1)
 {
     return make_hip_comp_func(std::make_shared<HipTCSC>(t, K, N, device));
+}
+// BlockedTCSC<B> (any class template over the block size with the same public
+// vectors): the more specialised overload, so the registration line reads as
+// for TCSC.
+template <template <int> class BlockedLike, int B>
+comp_func make_hip_comp_func(const BlockedLike<B> &t, int K, int N, int device = -1)
+{
+    return make_hip_comp_func(std::make_shared<HipTCSC>(HipTCSC::Blocked{}, t, K, N, B, device));
 }
 inline comp_func_prelu make_hip_comp_func_prelu(std::shared_ptr<HipTCSC> w)
 {

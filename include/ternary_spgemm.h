@@ -72,6 +72,18 @@ int tcsc_hip_encode_dense_dev(const int32_t *dW, int K, int N, int32_t *d_csp, i
 int tcsc_hip_create_csc_packed(const int32_t *col_ptr, const int32_t *row_idx,
                                const uint8_t *packed, int K, int N, int device, tsg_tcsc **out);
 
+/* BlockedTCSC<B> registration (data_structures/BlockedTCSC.h:5-49; the
+ * reference's main.cpp:69 builds it with B = BLOCK_SIZE = 512): col_start_pos /
+ * col_start_neg have (K/B)*N + 1 entries, slot kb*N + n listing column n's
+ * +1 / -1 rows of block kb ([kb*B, kb*B + B), ascending); rows past (K/B)*B
+ * are not part of the format.  Calls through the handle then compute
+ * BaseBlockedTCSC<float> (comp.h:607-658): per block y = 0 + pos - neg, Y += y
+ * block by block, then + b -- bit for bit, in that order.  Runs on the
+ * weight-compiled kernel only (TSG_KERNEL must be unset or "jit"). */
+int tcsc_hip_create_blocked(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                            const int32_t *row_index_pos, const int32_t *row_index_neg,
+                            int K, int N, int B, int device, tsg_tcsc **out);
+
 /* Releases every device/host resource of the handle (NULL is a no-op). */
 void tcsc_hip_destroy(tsg_tcsc *h);
 
@@ -176,6 +188,17 @@ int tsg_jit_codegen(const int32_t *col_start_pos, const int32_t *col_start_neg,
                     const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
                     uint32_t *code, int64_t code_cap, int64_t *code_len,
                     uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+/* Same for BlockedTCSC<B> arrays (tcsc_hip_create_blocked); B = 0 is plain TCSC. */
+int tsg_jit_codegen_blocked(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                            const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                            int B, uint32_t *code, int64_t code_cap, int64_t *code_len,
+                            uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+
+/* Checks BlockedTCSC<B> arrays (layout as tcsc_hip_create_blocked): monotone
+ * column starts, every row inside its block, ascending, no row both +1 and -1. */
+int tsg_blocked_tcsc_validate(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                              const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                              int B);
 
 /* X[i] = integer-valued fp32 U{-range..range} (initX, sparseUtils.h:6-23). */
 int tsg_gen_x(int64_t len, int range, uint64_t seed, float *X);

@@ -163,10 +163,10 @@ def tcsc_encode(W: np.ndarray) -> TCSC:
 
 
 def blocked_tcsc_encode(W: np.ndarray, B: int):
-    """BlockedTCSC<B> ctor (BlockedTCSC.h:15-41)."""
+    """BlockedTCSC<B> ctor (BlockedTCSC.h:15-41): K/B whole blocks; rows past
+    (K/B)*B are not encoded (BlockedTCSC.h:17)."""
     W = np.ascontiguousarray(W, dtype=np.int32)
     K, N = W.shape
-    assert K % B == 0
     p, q = _i64(), _i64()
     lib().oracle_tcsc_count(W, K, N, C.byref(p), C.byref(q))
     nslot = (K // B) * N + 1
@@ -175,7 +175,7 @@ def blocked_tcsc_encode(W: np.ndarray, B: int):
     rip = np.empty(max(p.value, 1), np.int32)
     rin = np.empty(max(q.value, 1), np.int32)
     lib().oracle_blocked_tcsc_encode(W, K, N, B, csp, csn, rip, rin)
-    return csp, csn, rip[: p.value].copy(), rin[: q.value].copy()
+    return csp, csn, rip[: csp[-1]].copy(), rin[: csn[-1]].copy()
 
 
 def csc_packed_encode(W: np.ndarray):

@@ -30,6 +30,7 @@ static int fail(int code, const std::string &msg)
 
 struct tsg_tcsc {
     int K = 0, N = 0, device = 0;
+    int B = 0;                            // BlockedTCSC<B> block size (0: plain TCSC)
     int64_t nnz_pos = 0, nnz_neg = 0;
     // kernel family: TSG_KERNEL=chunked (round-1 v1), pair / flat (LDS-gather
     // stream kernel, two walks), rx (register-X kernel), jit (weight-compiled)
@@ -158,6 +159,13 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     if (rc) return rc;
     int Mp, Kp;
     dims_for(h, M, Mp, Kp);
+    if (h->kind == tsg_tcsc::kJit) {
+        // the stream steps through X^T chunks with a 32-bit stride, and the grid
+        // (one workgroup per M tile x column tile) must stay under 2^32 threads
+        const int64_t wgs = (int64_t)(Mp / tsg::kJitTileM) * (h->jimg.Npad / tsg::kJitTileCols);
+        if ((int64_t)Mp * tsg::kJitChunk * 4 >= (1ll << 31) || wgs * tsg::kJitWaves * 64 >= (1ll << 32))
+            return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " is too large for one jit launch; split the rows");
+    }
     if (K == 0) {
         // no X at all: chain is +0; X^T stays zero
         HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
@@ -300,13 +308,20 @@ extern "C" int tcsc_hip_device_count(int *count)
     return TSG_OK;
 }
 
-extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                               const int32_t *rin, int K, int N, int device, tsg_tcsc **out)
+namespace {
+
+// Registration of TCSC (B = 0) or BlockedTCSC<B> arrays.
+int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
+                int B, int device, tsg_tcsc **out)
 {
     if (!out) return fail(TSG_ERR_ARG, "null out");
     *out = nullptr;
-    std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N);
-    if (!e.empty()) return fail(TSG_ERR_ARG, "malformed TCSC: " + e);
+    if (B < 0) return fail(TSG_ERR_ARG, "negative block size");
+    std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, B);
+    if (!e.empty()) return fail(TSG_ERR_ARG, std::string(B ? "malformed BlockedTCSC: " : "malformed TCSC: ") + e);
+    if (B && tsg::kJitSlots - tsg::kJitNW / 2 < 4)
+        return fail(TSG_ERR_ARG, "BlockedTCSC: this jit kernel geometry has no registers for the block sums");
+    const int64_t slots = (B ? (int64_t)(K / B) : 1) * N;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TSG_ERR_NODEV, "no HIP device");
     if (device < 0) HIP_TRY(hipGetDevice(&device));
@@ -317,17 +332,33 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     tsg_tcsc *h = new tsg_tcsc();
     h->K = K;
     h->N = N;
+    h->B = B;
     h->device = device;
-    h->nnz_pos = csp[N];
-    h->nnz_neg = csn[N];
-    h->csp.assign(csp, csp + N + 1);
-    h->csn.assign(csn, csn + N + 1);
+    h->nnz_pos = csp[slots];
+    h->nnz_neg = csn[slots];
+    h->csp.assign(csp, csp + slots + 1);
+    h->csn.assign(csn, csn + slots + 1);
     if (h->nnz_pos) h->rip.assign(rip, rip + h->nnz_pos);
     if (h->nnz_neg) h->rin.assign(rin, rin + h->nnz_neg);
     // kernel family (default: the weight-compiled kernel); TSG_KERNEL selects
     // the others for A/B and their own tests
     const char *kenv = std::getenv("TSG_KERNEL");
-    const std::string kname = kenv ? kenv : "jit";
+    // The weight-compiled image costs ~8 B per nonzero plus ~15% schedule code;
+    // stream offsets are 32-bit, so a W whose image would pass ~3 GiB (e.g.
+    // K=16384, N=131072, s=4 on ONE GPU -- shard columns instead)
+    // defaults to the rx kernel.  Asking for jit explicitly is then an error.
+    const double jit_est = 8.0 * 1.25 * ((double)h->nnz_pos + (double)h->nnz_neg);
+    const bool jit_fits = jit_est < 3.0 * (double)(1ull << 30);
+    const std::string kname = kenv ? kenv : (jit_fits ? "jit" : "rx");
+    if (B && kname != "jit") {
+        delete h;
+        return fail(TSG_ERR_ARG, "BlockedTCSC runs on the jit kernel only (TSG_KERNEL=" + kname + ")");
+    }
+    if (kname == "jit" && !jit_fits) {
+        delete h;
+        return fail(TSG_ERR_ARG, "TSG_KERNEL=jit: W has too many nonzeros for one weight-compiled image "
+                                 "(> ~300M); shard columns across handles or use TSG_KERNEL=rx");
+    }
     if (kname == "jit") h->kind = tsg_tcsc::kJit;
     else if (kname == "rx") h->kind = tsg_tcsc::kRx;
     else if (kname == "chunked") h->kind = tsg_tcsc::kChunked;
@@ -340,7 +371,7 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     const std::vector<uint32_t> *segv, *entv;
     static const std::vector<uint32_t> kNoEntries(1, 0u);
     if (h->kind == tsg_tcsc::kJit) {
-        tsg::build_jit_code(csp, csn, rip, rin, K, N, h->jimg);
+        tsg::build_jit_code(csp, csn, rip, rin, K, N, B, h->jimg);
         h->jit_code_bytes = (int64_t)h->jimg.code.size() * 4;
         DeviceGuard g0(device);
         const std::string err = h->jmod.load(h->jimg.code);
@@ -392,6 +423,24 @@ extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int
     }
     *out = h;
     return TSG_OK;
+}
+
+}  // namespace
+
+extern "C" int tcsc_hip_create(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                               const int32_t *rin, int K, int N, int device, tsg_tcsc **out)
+{
+    return create_impl(csp, csn, rip, rin, K, N, 0, device, out);
+}
+
+extern "C" int tcsc_hip_create_blocked(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                                       const int32_t *rin, int K, int N, int B, int device, tsg_tcsc **out)
+{
+    if (B <= 0) {
+        if (out) *out = nullptr;
+        return fail(TSG_ERR_ARG, "block size must be positive");
+    }
+    return create_impl(csp, csn, rip, rin, K, N, B, device, out);
 }
 
 extern "C" int tcsc_hip_create_dense(const int32_t *W, int K, int N, int device, tsg_tcsc **out)
@@ -508,7 +557,8 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     o->abi_version = TSG_ABI_VERSION;
     o->nnz_pos = h->nnz_pos;
     o->nnz_neg = h->nnz_neg;
-    o->tcsc_bytes = 4 * (2 * ((int64_t)h->N + 1) + h->nnz_pos + h->nnz_neg);
+    // TCSC / BlockedTCSC getDataStructureSize (TCSC.h:43-49, BlockedTCSC.h:43-47)
+    o->tcsc_bytes = 4 * (2 * (int64_t)h->csp.size() + h->nnz_pos + h->nnz_neg);
     const bool rx = h->kind == tsg_tcsc::kRx || h->kind == tsg_tcsc::kJit;
     o->image_bytes = h->kind == tsg_tcsc::kJit ? h->jit_code_bytes + (int64_t)h->jimg.wcode.size() * 4
                      : rx ? (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4
@@ -537,9 +587,11 @@ extern "C" int tcsc_hip_to_dense(const tsg_tcsc *h, int32_t *W, int K, int N)
 {
     if (!h || !W || K != h->K || N != h->N) return fail(TSG_ERR_ARG, "bad to_dense arguments");
     std::memset(W, 0, sizeof(int32_t) * (size_t)K * N);
-    for (int n = 0; n < N; n++) {
-        for (int32_t i = h->csp[n]; i < h->csp[n + 1]; i++) W[(size_t)h->rip[i] * N + n] = 1;
-        for (int32_t i = h->csn[n]; i < h->csn[n + 1]; i++) W[(size_t)h->rin[i] * N + n] = -1;
+    const size_t slots = h->csp.size() - 1;  // N, or (K/B)*N for BlockedTCSC (slot s: column s % N)
+    for (size_t s = 0; s < slots; s++) {
+        const size_t n = s % (size_t)N;
+        for (int32_t i = h->csp[s]; i < h->csp[s + 1]; i++) W[(size_t)h->rip[i] * N + n] = 1;
+        for (int32_t i = h->csn[s]; i < h->csn[s + 1]; i++) W[(size_t)h->rin[i] * N + n] = -1;
     }
     return TSG_OK;
 }

@@ -240,32 +240,40 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 }
 
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                          const int32_t *rin, int K, int N)
+                          const int32_t *rin, int K, int N, int B)
 {
     if (K < 0 || N < 0) return "negative K or N";
+    if (B < 0) return "negative block size";
     if (!csp || !csn) return "null col_start array";
+    // plain TCSC: one slot per column, rows in [0, K); BlockedTCSC<B>
+    // (BlockedTCSC.h:15-41): slot kb*N + n holds column n's rows of block kb,
+    // [kb*B, kb*B + B), for the K/B whole blocks
+    const int64_t nb = B ? K / B : 1, slots = nb * N;
     if (csp[0] != 0 || csn[0] != 0) return "col_start[0] must be 0";
-    for (int n = 0; n < N; n++) {
-        if (csp[n + 1] < csp[n]) return "col_start_pos not monotone at n=" + std::to_string(n);
-        if (csn[n + 1] < csn[n]) return "col_start_neg not monotone at n=" + std::to_string(n);
+    for (int64_t s = 0; s < slots; s++) {
+        if (csp[s + 1] < csp[s]) return "col_start_pos not monotone at slot " + std::to_string(s);
+        if (csn[s + 1] < csn[s]) return "col_start_neg not monotone at slot " + std::to_string(s);
     }
-    if ((csp[N] > 0 && !rip) || (csn[N] > 0 && !rin)) return "null row_index array";
-    for (int n = 0; n < N; n++) {
+    if ((csp[slots] > 0 && !rip) || (csn[slots] > 0 && !rin)) return "null row_index array";
+    for (int64_t s = 0; s < slots; s++) {
+        const int n = (int)(s % (N ? N : 1));
+        const int64_t klo = B ? (s / N) * B : 0, khi = B ? klo + B : K;
+        const std::string where = B ? "block " + std::to_string(s / N) + " column " + std::to_string(n)
+                                    : "column " + std::to_string(n);
         for (int p = 0; p < 2; p++) {
             const int32_t *cs = p ? csn : csp;
             const int32_t *ri = p ? rin : rip;
-            for (int32_t i = cs[n]; i < cs[n + 1]; i++) {
-                if (ri[i] < 0 || ri[i] >= K)
-                    return "row index out of [0,K) in column " + std::to_string(n);
-                if (i > cs[n] && ri[i] <= ri[i - 1])
-                    return "row indices not strictly ascending in column " + std::to_string(n);
+            for (int32_t i = cs[s]; i < cs[s + 1]; i++) {
+                if (ri[i] < klo || ri[i] >= khi)
+                    return (B ? "row index out of its block in " : "row index out of [0,K) in ") + where;
+                if (i > cs[s] && ri[i] <= ri[i - 1]) return "row indices not strictly ascending in " + where;
             }
         }
         // a k may not be both +1 and -1 in one column (the format encodes a
         // single ternary value per (k, n))
-        int32_t a = csp[n], b = csn[n];
-        while (a < csp[n + 1] && b < csn[n + 1]) {
-            if (rip[a] == rin[b]) return "row index in both +1 and -1 runs of column " + std::to_string(n);
+        int32_t a = csp[s], b = csn[s];
+        while (a < csp[s + 1] && b < csn[s + 1]) {
+            if (rip[a] == rin[b]) return "row index in both +1 and -1 runs of " + where;
             if (rip[a] < rin[b]) a++; else b++;
         }
     }
@@ -295,6 +303,21 @@ static inline uint64_t below(uint64_t &s, uint64_t n)
 // ---------------------------------------------------------------- C-ABI --
 
 thread_local std::string g_tsg_host_err;
+
+extern "C" int tsg_blocked_tcsc_validate(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                                         const int32_t *rin, int K, int N, int B)
+{
+    if (B <= 0) {
+        g_tsg_host_err = "block size must be positive";
+        return TSG_ERR_ARG;
+    }
+    const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, B);
+    if (!e.empty()) {
+        g_tsg_host_err = e;
+        return TSG_ERR_ARG;
+    }
+    return TSG_OK;
+}
 
 extern "C" int tsg_tcsc_validate(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                                  const int32_t *rin, int K, int N)

@@ -138,12 +138,14 @@ constexpr int kJitSlots = TSG_JIT_GEOM == 2 ? 24 : 48;  // X slot registers v[8 
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
 
 struct JitImage {
-    int K = 0, N = 0, Npad = 0, nch = 0;
+    int K = 0, N = 0, Npad = 0, nch = 0, B = 0;
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
     std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
 };
+// B = 0: BaseTCSC order (comp.h:25-69); B > 0: BaseBlockedTCSC<B> order
+// (comp.h:607-658) from BlockedTCSC<B> arrays
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                    const int32_t *rin, int K, int N, JitImage &img);
+                    const int32_t *rin, int K, int N, int B, JitImage &img);
 
 struct JitModule {
     void *module = nullptr;        // hipModule_t
@@ -171,8 +173,9 @@ void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                  const int32_t *rin, int K, int N, int tile_cols, Image &img);
 int pick_tile_cols(int N);
 
+// B = 0: plain TCSC; B > 0: BlockedTCSC<B> arrays ((K/B)*N + 1 column starts)
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                          const int32_t *rin, int K, int N);
+                          const int32_t *rin, int K, int N, int B = 0);
 
 // GPU-side TCSC encoder (csrc/tsg_encode.hip).  encode_count: column starts
 // into d_csp/d_csn (N+1 each); with d_tmp == nullptr it only returns the scan

@@ -45,6 +45,21 @@ struct Emit {
         c.push_back(0xd3b24000u | d | (neg ? 0x200u : 0u));
         c.push_back((3u << 27) | ((256u + x) << 9) | (256u + d) | (neg ? (2u << 29) : 0u));
     }
+    // v_pk_add_f32 v[d:d+1], [-]v[x:x+1], 0: the first entry of a BlockedTCSC
+    // block, 0 + x (resp. 0 - x) as one IEEE add per half
+    void pk_first(uint32_t d, uint32_t x, bool neg)
+    {
+        align8();
+        c.push_back(0xd3b24000u | d | (neg ? 0x100u : 0u));
+        c.push_back((3u << 27) | (128u << 9) | (256u + x) | (neg ? (1u << 29) : 0u));
+    }
+    // v_pk_add_f32 v[d:d+1], v[d:d+1], v[t:t+1]: Y += y of a finished block
+    void pk_acc(uint32_t d, uint32_t t)
+    {
+        align8();
+        c.push_back(0xd3b24000u | d);
+        c.push_back((3u << 27) | ((256u + t) << 9) | (256u + d));
+    }
     // ds_read_b64 v[d:d+1], v[a] offset:off
     void ds_read_b64(uint32_t d, uint32_t a, uint32_t off)
     {
@@ -115,27 +130,75 @@ struct Section {
     std::vector<std::vector<uint8_t>> cols;
 };
 
+// One step of a stream: the X^T chunk staged into LDS buffer q % 3 and which
+// of its entries the step adds.
+struct StepSpec {
+    int chunk;       // X^T chunk (kJitChunk rows)
+    int pass;        // 0: +1 entries, 1: -1 entries
+    int c0, c1;      // the wave's columns [c0, c1)
+    int klo, khi;    // rows the step consumes (a BlockedTCSC block may end inside the chunk)
+    int64_t slot0;   // column n's entries are TCSC slot slot0 + n (BlockedTCSC: block * N)
+    bool reset;      // first step of a (block, pass) run: the entry cursors restart at the slots
+    bool flush;      // BlockedTCSC: the block's last step: Y += y for its columns
+};
+
+// BaseTCSC (comp.h:37-63): pass 0 over every chunk, then pass 1; the wave's
+// columns accumulate in place.
+// BaseBlockedTCSC (comp.h:620-646): per block y = 0 + pos - neg, then
+// Y += y.  y of every column of a block is live across the block's chunks, so
+// a wave runs its columns in two halves (y of half the columns in the upper
+// X-slot registers); per half, block by block: pass 0 over the chunks the
+// block touches, pass 1, then Y += y.
+std::vector<StepSpec> plan_steps(int K, int N, int B, int nch)
+{
+    std::vector<StepSpec> plan;
+    const int C = kJitChunk;
+    if (!B) {
+        for (int p = 0; p < 2; p++)
+            for (int j = 0; j < nch; j++) plan.push_back({j, p, 0, kJitNW, j * C, j * C + C, 0, j == 0, false});
+        return plan;
+    }
+    const int nb = K / B, half = kJitNW / 2;  // rows past nb * B are not in the format (BlockedTCSC.h:17)
+    for (int h = 0; h < 2; h++)
+        for (int kb = 0; kb < nb; kb++) {
+            const int r0 = kb * B, r1 = r0 + B, jlo = r0 / C, jhi = (r1 - 1) / C;
+            for (int p = 0; p < 2; p++)
+                for (int j = jlo; j <= jhi; j++)
+                    plan.push_back({j, p, h * half, h * half + half, std::max(r0, j * C), std::min(r1, j * C + C),
+                                    (int64_t)kb * N, j == jlo, p == 1 && j == jhi});
+        }
+    return plan;
+}
+
 }  // namespace
 
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
-                    int K, int N, JitImage &img)
+                    int K, int N, int B, JitImage &img)
 {
     img.K = K;
     img.N = N;
+    img.B = B;
     img.Npad = ((N + kJitTileCols - 1) / kJitTileCols) * kJitTileCols;
     img.nch = std::max(1, (K + kJitChunk - 1) / kJitChunk);
-    const int nch = img.nch, ntiles = img.Npad / kJitTileCols, steps = 2 * nch;
+    const int nch = img.nch, ntiles = img.Npad / kJitTileCols;
+    const std::vector<StepSpec> plan = plan_steps(K, N, B, nch);
+    const int steps = (int)plan.size();
+    // X slots: all of v[8 : lds) for BaseTCSC; BlockedTCSC keeps y of half the
+    // columns (kJitNW registers) at the top of that range
+    const int S = B ? kJitSlots - kJitNW / 2 : kJitSlots;
+    const uint32_t kTmp0 = kXSlot0 + 2u * (uint32_t)S;  // y of column c0 + c: v[tmp0 + 2c : +1]
     img.wcode.assign((size_t)ntiles * kJitStreams, 0u);
     std::vector<uint32_t> &code = img.code;
     code.clear();
-    const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
-    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitStreams * (steps * 220 + 64) + kTailPad + 64);
+    const int64_t slots = (B ? (int64_t)(K / B) : 1) * N;
+    const int64_t nnz = (int64_t)csp[slots] + (int64_t)csn[slots];
+    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitStreams * ((size_t)steps * 220 + 64) + kTailPad + 64);
     // header: magic, then the geometry (tests/test_jit_codegen.py derives the
-    // register contract from it)
+    // register contract from it), the block size and the X slots in use
     code.insert(code.end(), {kJitMagic0, kJitMagic1,
                              (uint32_t)kJitWaves | (uint32_t)kJitNW << 8 | (uint32_t)kJitChunk << 16,
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
-                             (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, 0u, 0u, 0u});
+                             (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S, 0u});
     Emit E{code};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
@@ -148,16 +211,25 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     uint32_t touch_first = 1, touch_count = 2;
     if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
 
+    int n0 = 0;  // first column of the current stream
     std::vector<int32_t> cur((size_t)kJitNW * 2), end((size_t)kJitNW * 2);
-    // step q's section: consumes the wave's entries of chunk q % nch, pass q / nch
+    std::vector<uint8_t> live(kJitNW, 0);  // BlockedTCSC: y of the column holds an entry
+    // step q's section: consumes the wave's entries in rows [klo, khi) of its pass
     auto build_section = [&](int q, Section &sec) {
-        const int p = q / nch, klo = (q % nch) * kJitChunk, khi = klo + kJitChunk;
-        const int32_t *ri = p ? rin : rip;
+        const StepSpec &sp = plan[(size_t)q];
+        const int p = sp.pass, kc = sp.chunk * kJitChunk;
+        const int32_t *cs = p ? csn : csp, *ri = p ? rin : rip;
+        if (sp.reset)
+            for (int col = sp.c0; col < sp.c1; col++) {
+                const int n = n0 + col;
+                cur[(size_t)col * 2 + p] = n < N ? cs[sp.slot0 + n] : 0;
+                end[(size_t)col * 2 + p] = n < N ? cs[sp.slot0 + n + 1] : 0;
+            }
         std::vector<std::vector<uint8_t>> by_row(kJitChunk);
-        for (int col = 0; col < kJitNW; col++) {
+        for (int col = sp.c0; col < sp.c1; col++) {
             int32_t &i = cur[(size_t)col * 2 + p];
             const int32_t e = end[(size_t)col * 2 + p];
-            for (; i < e && ri[i] < khi; i++) by_row[ri[i] - klo].push_back((uint8_t)col);
+            for (; i < e && ri[i] < sp.khi; i++) by_row[ri[i] - kc].push_back((uint8_t)col);
         }
         sec.rows.clear();
         sec.cols.clear();
@@ -172,16 +244,12 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // piece, set by the dispatcher) + buffer + piece offset
     auto emit_dma = [&](int q) {
         if (d_nodma) return;
-        const int j = q % nch;
-        if (j == 0) {
+        const int j = plan[(size_t)q].chunk;
+        if (j == 0 || base_chunk < 0 || j < base_chunk) {
             E.base_reset();
+            for (int i = 0; i < j; i++) E.base_next();
         } else {
-            if (base_chunk != j - 1) {  // not reached: chunks are staged in order
-                E.base_reset();
-                for (int i = 0; i < j; i++) E.base_next();
-            } else {
-                E.base_next();
-            }
+            for (int i = base_chunk; i < j; i++) E.base_next();
         }
         base_chunk = j;
         E.nop(4);  // SALU-written SGPR base -> VMEM
@@ -193,7 +261,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     };
 
     // X row schedule.  The wave's used rows, over all steps, form one sequence
-    // g = 0, 1, ...; row g lives in X slot g % kJitSlots.  Rows are processed
+    // g = 0, 1, ...; row g lives in X slot g % S.  Rows are processed
     // in groups of G (never across a step): at a group's start the wave waits
     // (counted lgkmcnt; LDS returns in order) for the group's reads, then
     // issues the reads of the following rows up to RA rows past the group (at
@@ -201,32 +269,28 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // group's entries -- column by column (pairs interleaved) or row by row.
     // Every column meets its rows in ascending k either way.
     // TSG_JIT_READS="G,RA,order" (order 0 = column-major, 1 = row-major);
-    // default 24,24,0 (the block schedule: one group of reads in flight).
-    int G = kJitSlots / 2, RA = kJitSlots / 2, row_major = 0;
+    // default S/2,S/2,0 (the block schedule: one group of reads in flight).
+    int G = S / 2, RA = S / 2, row_major = 0;
     if (const char *rv = std::getenv("TSG_JIT_READS")) std::sscanf(rv, "%d,%d,%d", &G, &RA, &row_major);
-    if (G < 1 || RA < 0 || G + RA > kJitSlots) {
-        G = kJitSlots / 2;
-        RA = kJitSlots / 2;
+    if (G < 1 || RA < 0 || G + RA > S) {
+        G = S / 2;
+        RA = S / 2;
     }
     for (int t = 0; t < ntiles; t++) {
         for (int w = 0; w < kJitStreams; w++) {
             while (code.size() % 64) E.nop();  // 256-B aligned stream start
             img.wcode[(size_t)t * kJitStreams + w] = E.pos_bytes();
-            const int n0 = t * kJitTileCols + w * kJitNW;
-            for (int col = 0; col < kJitNW; col++)
-                for (int p = 0; p < 2; p++) {
-                    const int n = n0 + col;
-                    const int32_t *cs = p ? csn : csp;
-                    cur[(size_t)col * 2 + p] = n < N ? cs[n] : 0;
-                    end[(size_t)col * 2 + p] = n < N ? cs[n + 1] : 0;
-                }
+            n0 = t * kJitTileCols + w * kJitNW;
+            std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
             E.save_m0();
             // prologue: steps 0 and 1 staged, landed, visible
-            emit_dma(0);
-            emit_dma(1);
-            E.wait_vm0();
-            E.barrier();
+            if (steps > 0) {
+                emit_dma(0);
+                if (steps > 1) emit_dma(1);
+                E.wait_vm0();
+                E.barrier();
+            }
             std::vector<Section> secs(steps);
             std::vector<int64_t> first(steps + 1, 0);  // global index of each step's first row
             int built = 0;
@@ -247,7 +311,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     if (issued >= first[rq + 1]) return;  // past step qmax
                     const int r = secs[rq].rows[(size_t)(issued - first[rq])];
                     if (!d_noreads)
-                        E.ds_read_b64(kXSlot0 + 2u * (uint32_t)(issued % kJitSlots), kLdsBaseV + (uint32_t)(rq % 3),
+                        E.ds_read_b64(kXSlot0 + 2u * (uint32_t)(issued % S), kLdsBaseV + (uint32_t)(rq % 3),
                                       (uint32_t)r * kRowBytes);
                 }
             };
@@ -259,7 +323,23 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             };
             for (int q = 0; q < steps; q++) {
                 ensure(q + 1);
-                const bool neg = q / nch == 1;
+                const StepSpec &sp = plan[(size_t)q];
+                const bool neg = sp.pass == 1;
+                // one entry: BaseTCSC adds into the column's accumulator; a
+                // BlockedTCSC block chains in y (0 + first entry, then in place)
+                auto add = [&](int col, uint32_t x) {
+                    if (!B) {
+                        E.pk_add(kAcc0 + 2u * (uint32_t)col, x, neg);
+                        return;
+                    }
+                    const uint32_t d = kTmp0 + 2u * (uint32_t)(col - sp.c0);
+                    if (live[col]) {
+                        E.pk_add(d, x, neg);
+                    } else {
+                        E.pk_first(d, x, neg);
+                        live[col] = 1;
+                    }
+                };
                 if (q + 2 < steps) emit_dma(q + 2);
                 for (uint32_t d = 0; d < (d_notouch ? 0u : touch_count); d++) {
                     E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
@@ -270,30 +350,35 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 const int nrow = (int)sec.rows.size();
                 for (int i0 = 0; i0 < nrow; i0 += G) {
                     const int i1 = std::min(nrow, i0 + G);
-                    const int64_t g0 = first[q] + i0, g1 = first[q] + i1;
+                    const int64_t g1 = first[q] + i1;
                     issue_reads(g1, q);  // (only if the schedule left the group unread)
                     wait_rows(g1);
                     issue_reads(g1 + RA, q + 1);
                     if (row_major) {
                         for (int i = i0; i < i1; i++) {
-                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % kJitSlots);
-                            for (uint8_t col : sec.cols[i]) E.pk_add(kAcc0 + 2u * col, x, neg);
+                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % S);
+                            for (uint8_t col : sec.cols[i]) add(col, x);
                         }
                     } else {
                         // per column its entries of the group; columns in pairs, interleaved
                         std::vector<std::vector<uint32_t>> xs(kJitNW);
                         for (int i = i0; i < i1; i++) {
-                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % kJitSlots);
+                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % S);
                             for (uint8_t col : sec.cols[i]) xs[col].push_back(x);
                         }
-                        for (int col = 0; col < kJitNW; col += 2)
+                        for (int col = sp.c0; col < sp.c1; col += 2)
                             for (size_t k = 0; k < std::max(xs[col].size(), xs[col + 1].size()); k++) {
-                                if (k < xs[col].size()) E.pk_add(kAcc0 + 2u * col, xs[col][k], neg);
-                                if (k < xs[col + 1].size()) E.pk_add(kAcc0 + 2u * (col + 1), xs[col + 1][k], neg);
+                                if (k < xs[col].size()) add(col, xs[col][k]);
+                                if (k < xs[col + 1].size()) add(col + 1, xs[col + 1][k]);
                             }
                     }
-                    (void)g0;
                 }
+                if (sp.flush)  // comp.h:642: Y += y (a block without entries adds +0: a no-op, Y is never -0)
+                    for (int col = sp.c0; col < sp.c1; col++)
+                        if (live[col]) {
+                            E.pk_acc(kAcc0 + 2u * (uint32_t)col, kTmp0 + 2u * (uint32_t)(col - sp.c0));
+                            live[col] = 0;
+                        }
                 issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first rows
                 E.wait_vm0();
                 if (!d_nobar) E.barrier();
@@ -417,17 +502,22 @@ int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t
 // ---------------------------------------------------------------- C-ABI --
 extern thread_local std::string g_tsg_host_err;
 
-extern "C" int tsg_jit_codegen(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                               const int32_t *rin, int K, int N, uint32_t *code, int64_t code_cap,
-                               int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
+extern "C" int tsg_jit_codegen_blocked(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                                       const int32_t *rin, int K, int N, int B, uint32_t *code,
+                                       int64_t code_cap, int64_t *code_len, uint32_t *wcode, int64_t wcode_cap,
+                                       int64_t *wcode_len)
 {
-    const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N);
+    const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, B);
     if (!e.empty()) {
-        g_tsg_host_err = "tsg_jit_codegen: malformed TCSC: " + e;
+        g_tsg_host_err = std::string(B ? "tsg_jit_codegen: malformed BlockedTCSC: " : "tsg_jit_codegen: malformed TCSC: ") + e;
+        return TSG_ERR_ARG;
+    }
+    if (B && tsg::kJitSlots - tsg::kJitNW / 2 < 4) {
+        g_tsg_host_err = "tsg_jit_codegen: this kernel geometry has no registers for BlockedTCSC";
         return TSG_ERR_ARG;
     }
     tsg::JitImage img;
-    tsg::build_jit_code(csp, csn, rip, rin, K, N, img);
+    tsg::build_jit_code(csp, csn, rip, rin, K, N, B, img);
     if (code_len) *code_len = (int64_t)img.code.size();
     if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
     if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
@@ -437,4 +527,12 @@ extern "C" int tsg_jit_codegen(const int32_t *csp, const int32_t *csn, const int
     if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);
     if (wcode) std::memcpy(wcode, img.wcode.data(), img.wcode.size() * 4);
     return TSG_OK;
+}
+
+extern "C" int tsg_jit_codegen(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                               const int32_t *rin, int K, int N, uint32_t *code, int64_t code_cap,
+                               int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
+{
+    return tsg_jit_codegen_blocked(csp, csn, rip, rin, K, N, 0, code, code_cap, code_len, wcode, wcode_cap,
+                                   wcode_len);
 }

@@ -35,6 +35,28 @@ struct HostTCSC {  // same public layout as class TCSC (TCSC.h:5-11)
     std::vector<int> col_start_pos, col_start_neg, row_index_pos, row_index_neg;
 };
 
+// Same public layout as BlockedTCSC<B> (BlockedTCSC.h:7-13), built from the
+// TCSC: slot kb*N + n = column n's rows of block kb, K/B whole blocks.
+template <int B>
+struct HostBlockedTCSC {
+    std::vector<int> col_start_pos, col_start_neg, row_index_pos, row_index_neg;
+    HostBlockedTCSC(const HostTCSC &t, int K, int N)
+    {
+        for (int kb = 0; kb < K / B; kb++)
+            for (int n = 0; n < N; n++) {
+                col_start_pos.push_back((int)row_index_pos.size());
+                col_start_neg.push_back((int)row_index_neg.size());
+                for (int i = t.col_start_pos[n]; i < t.col_start_pos[n + 1]; i++)
+                    if (t.row_index_pos[i] / B == kb) row_index_pos.push_back(t.row_index_pos[i]);
+                for (int i = t.col_start_neg[n]; i < t.col_start_neg[n + 1]; i++)
+                    if (t.row_index_neg[i] / B == kb) row_index_neg.push_back(t.row_index_neg[i]);
+            }
+        col_start_pos.push_back((int)row_index_pos.size());
+        col_start_neg.push_back((int)row_index_neg.size());
+    }
+};
+constexpr int kBlockSize = 512;  // BLOCK_SIZE, main.cpp:7
+
 // Dense reference GEMM (the driver's own check, as sparseUtils.h:92-108 is the
 // reference driver's): y = sum_k X[m,k]*W[k,n]; Y = y + b[n].
 static void dense_gemm(const float *X, const int *W, const float *b, float *Y, int M, int N, int K)
@@ -91,6 +113,10 @@ int main(int argc, char **argv)
 
     auto hw = std::make_shared<tsg::HipTCSC>(W, K, N);
     add_function(tsg::make_hip_comp_func(hw), "HipBaseTCSC");
+    // BaseBlockedTCSC over BlockedTCSC<512> (main.cpp:69,84-88), where K is a
+    // whole number of blocks ("ASSUMING K DIVIDES B", BlockedTCSC.h:5)
+    if (K >= kBlockSize && K % kBlockSize == 0)
+        add_function(tsg::make_hip_comp_func(HostBlockedTCSC<kBlockSize>(W, K, N), K, N), "HipBaseBlockedTCSC");
     std::printf("%zu regular functions and 0 PrelU functions registered.\n", userFuncs.size());
 
     std::vector<float> X((size_t)M * K + 10), B(N, 2.0f), Y((size_t)M * N + 10, 0.0f);

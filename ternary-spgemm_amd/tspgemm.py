@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_last_error", "tcsc_hip_device_count", "tsg_tcsc_slice", "tsg_tcsc_validate",
     "tsg_gen_tcsc", "tsg_gen_x", "tcsc_hip_create_csc_packed", "tsg_tcsc_to_csc_packed",
     "tsg_csc_packed_to_tcsc", "tsg_jit_codegen", "tcsc_hip_kernel_name", "tcsc_hip_encode_dense_dev",
+    "tcsc_hip_create_blocked", "tsg_jit_codegen_blocked", "tsg_blocked_tcsc_validate",
 )
 
 
@@ -82,6 +83,7 @@ def lib() -> C.CDLL:
     H = C.c_void_p
     L.tcsc_hip_create.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.POINTER(H)]
     L.tcsc_hip_create_dense.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(H)]
+    L.tcsc_hip_create_blocked.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(H)]
     L.tcsc_hip_destroy.argtypes = [H]
     L.tcsc_hip_destroy.restype = None
     L.tcsc_hip_gemm.argtypes = [H, vp, vp, vp, C.c_int, C.c_int, C.c_int]
@@ -103,6 +105,7 @@ def lib() -> C.CDLL:
     L.tsg_tcsc_slice.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp,
                                  C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.tsg_tcsc_validate.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int]
+    L.tsg_blocked_tcsc_validate.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int]
     L.tsg_gen_tcsc.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
                                vp, vp, vp, vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.tsg_gen_x.argtypes = [C.c_int64, C.c_int, C.c_uint64, vp]
@@ -112,6 +115,8 @@ def lib() -> C.CDLL:
                                          C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.tsg_jit_codegen.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
                                   C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
+    L.tsg_jit_codegen_blocked.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
+                                          C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     for f in EXPORTED_SYMBOLS:
         if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name"):
             getattr(L, f).restype = C.c_int
@@ -207,20 +212,28 @@ def csc_packed_to_tcsc(col_ptr, row_idx, packed, N: int):
     return o[0], o[1], o[2][: p.value], o[3][: q.value]
 
 
-def jit_codegen(csp, csn, rip, rin, K: int, N: int):
+def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0):
     """Host-side machine code of the weight-compiled kernel (TSG_KERNEL=jit):
-    (region words uint32[], per-(tile, wave) stream byte offsets uint32[])."""
+    (region words uint32[], per-(tile, wave) stream byte offsets uint32[]).
+    B > 0: the arrays are BlockedTCSC<B> (tcsc_hip_create_blocked)."""
     csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
     nc, nw = C.c_int64(), C.c_int64()
     L = lib()
-    _check(L.tsg_jit_codegen(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, None, 0,
-                             C.byref(nc), None, 0, C.byref(nw)), "tsg_jit_codegen")
+    _check(L.tsg_jit_codegen_blocked(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B, None, 0,
+                                     C.byref(nc), None, 0, C.byref(nw)), "tsg_jit_codegen")
     code = np.empty(nc.value, np.uint32)
     wcode = np.empty(nw.value, np.uint32)
-    _check(L.tsg_jit_codegen(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, _ptr(code),
-                             nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
+    _check(L.tsg_jit_codegen_blocked(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B, _ptr(code),
+                                     nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
            "tsg_jit_codegen")
     return code, wcode
+
+
+def validate_blocked(csp, csn, rip, rin, K: int, N: int, B: int) -> None:
+    """Raises TSGError unless the arrays are a well-formed BlockedTCSC<B>."""
+    csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
+    _check(lib().tsg_blocked_tcsc_validate(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B),
+           "tsg_blocked_tcsc_validate")
 
 
 def encode_dense_torch(W):
@@ -283,6 +296,20 @@ class TCSCDevice:
         h = C.c_void_p()
         _check(lib().tcsc_hip_create_csc_packed(_ptr(col_ptr), _ptr(row_idx), _ptr(packed), K, N,
                                                 device, C.byref(h)), "tcsc_hip_create_csc_packed")
+        self._h = h
+        return self
+
+    @classmethod
+    def from_blocked(cls, csp, csn, rip, rin, K: int, N: int, B: int,
+                     device: int = -1) -> "TCSCDevice":
+        """BlockedTCSC<B> arrays (BlockedTCSC.h:15-41): calls compute
+        BaseBlockedTCSC (comp.h:607-658) bit for bit (tcsc_hip_create_blocked)."""
+        csp, csn, rip, rin = map(_i32, (csp, csn, rip, rin))
+        self = cls.__new__(cls)
+        self.K, self.N = int(K), int(N)
+        h = C.c_void_p()
+        _check(lib().tcsc_hip_create_blocked(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), self.K, self.N,
+                                             int(B), device, C.byref(h)), "tcsc_hip_create_blocked")
         self._h = h
         return self
 

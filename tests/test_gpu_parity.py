@@ -251,3 +251,52 @@ def test_gpu_encoder_matches_host_ctor(tsg, oracle_mod):
     X = O.init_x_frac(77, 700, 1)
     b = np.linspace(-1, 1, 300).astype(np.float32)
     assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, O.tcsc_encode(W), b))
+
+
+@pytest.mark.parametrize("M,K,N,s,B", [(5, 70, 33, 2, 16), (130, 1000, 520, 4, 64), (17, 300, 64, 8, 100),
+                                       (131, 1100, 700, 4, 512), (9, 96, 70, 2, 1), (4, 10, 5, 2, 32),
+                                       (256, 4096, 1024, 4, 512)])
+def test_blocked_tcsc_vs_oracle(tsg, oracle_mod, M, K, N, s, B):
+    """BlockedTCSC<B> (BlockedTCSC.h:15-41) registered as is, BaseBlockedTCSC
+    (comp.h:607-658) order bit for bit: integer X (== BaseTCSC / the dense GEMM,
+    SURVEY 8f rank 2's pin) and order-sensitive X.  B = 512 is the reference's
+    BLOCK_SIZE (main.cpp:7); K % B != 0 drops the tail rows as the ctor does."""
+    O = oracle_mod
+    W = O.gen_ternary(K, N, s, M + K + B)
+    blk = O.blocked_tcsc_encode(W, B)
+    h = tsg.TCSCDevice.from_blocked(*blk, K, N, B)
+    assert h.kernel_name() == "tsg_jit_kernel"
+    Wt = W.copy()
+    Wt[(K // B) * B:] = 0
+    assert np.array_equal(h.to_dense(), Wt)
+    assert h.info()["tcsc_bytes"] == 4 * (len(blk[0]) + len(blk[1]) + len(blk[2]) + len(blk[3]))
+    b = np.linspace(-2, 2, N).astype(np.float32)
+    Xi, Xf = O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)
+    assert _bits_eq(h.gemm(Xi, b), O.base_blocked_tcsc(Xi, blk, b, K, N, B))
+    assert _bits_eq(h.gemm(Xi, b), O.base_tcsc(Xi, O.tcsc_encode(Wt), b))
+    assert _bits_eq(h.gemm(Xf, b), O.base_blocked_tcsc(Xf, blk, b, K, N, B))
+    h.close()
+
+
+def test_blocked_tcsc_kat(tsg, oracle_mod):
+    """plots/data_example_image/blocked.py:12-30 (4x4, B = 2)."""
+    O = oracle_mod
+    kat = json.load(open(os.path.join(GOLDEN, "kat_blocked_4x4_B2.json")))
+    W = np.array(kat["W"], np.int32)
+    blk = O.blocked_tcsc_encode(W, 2)
+    h = tsg.TCSCDevice.from_blocked(*blk, 4, 4, 2)
+    X = np.array(kat["X"], np.float32)
+    b = np.zeros(4, np.float32)
+    assert _bits_eq(h.gemm(X, b), O.base_blocked_tcsc(X, blk, b, 4, 4, 2))
+
+
+def test_blocked_tcsc_errors(tsg, oracle_mod, monkeypatch):
+    O = oracle_mod
+    blk = O.blocked_tcsc_encode(O.gen_ternary(64, 8, 2, 1), 16)
+    with pytest.raises(tsg.TSGError):
+        tsg.TCSCDevice.from_blocked(*blk, 64, 8, 0)
+    with pytest.raises(tsg.TSGError, match="malformed BlockedTCSC"):
+        tsg.TCSCDevice.from_blocked(*blk, 64, 8, 32)  # arrays are for B = 16
+    monkeypatch.setenv("TSG_KERNEL", "rx")
+    with pytest.raises(tsg.TSGError, match="jit kernel only"):
+        tsg.TCSCDevice.from_blocked(*blk, 64, 8, 16)

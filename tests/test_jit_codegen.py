@@ -37,13 +37,21 @@ class Geom:
         self.dma_v = self.sink_v + 1
         self.l128_v = self.dma_v + self.pieces
         self.acc0 = (self.l128_v + 2) & ~1
+        # BlockedTCSC<B> (B > 0): X slots v[8 : 8 + 2 xslots), block sums y above them
+        self.B = int(code[5])
+        self.xslots = int(code[6]) or self.slots
+        self.tmp0 = 8 + 2 * self.xslots
+
+
 XT_BASE = 1 << 40  # fake device address of X^T
 
 
 class Wave:
     def __init__(self, w, pc):
         self.w, self.pc = w, pc
-        self.v = np.zeros((256, 64), np.float32)
+        # registers the dispatcher does not set hold garbage: NaN poisons any
+        # use before a def; the accumulators start at +0 (tsg_jit_kernel.hip)
+        self.v = np.full((256, 64), np.nan, np.float32)
         self.m0 = 0x5A5A
         self.saved_m0 = None
         self.base = None
@@ -51,6 +59,31 @@ class Wave:
         self.pending = []  # DMA copies not yet landed: (lds_byte, data, issue_phase)
         self.reads = []    # X slot registers of LDS reads not yet waited for, oldest first
         self.done = False
+
+
+def _classify_pk(w0, w1, G):
+    """v_pk_add_f32 forms the generator may emit (tsg_jit.cpp Emit):
+    add   v[d] = v[d] +/- X slot      (d: accumulator; BlockedTCSC: block sum y)
+    first v[d] = +/-X slot + 0        (BlockedTCSC: a block's first entry, 0 + x / 0 - x)
+    flush v[d] = v[d] + y             (BlockedTCSC: Y += y at a block's end)"""
+    d = w0 & 0xFF
+    neg0, neg1 = bool(w0 & 0x100), bool(w0 & 0x200)  # neg_hi of src0 / src1
+    assert (w1 >> 29) & 1 == neg0 and (w1 >> 30) & 1 == neg1, "neg_lo and neg_hi disagree"
+    assert (w1 >> 18) & 0x1FF == 0 and (w1 >> 27) & 3 == 3 and (w0 >> 11) & 0x1F == 8  # op_sel_hi, clamp/opsel
+    s0, s1 = w1 & 0x1FF, (w1 >> 9) & 0x1FF
+    x_lo, x_hi = 8, 8 + 2 * G.xslots
+    acc = G.acc0 <= d < G.acc0 + 2 * G.nw
+    tmp = G.B and G.tmp0 <= d < G.tmp0 + G.nw
+    assert d % 2 == 0
+    if s1 == 128:  # inline constant 0
+        assert tmp and not neg1 and x_lo <= s0 - 256 < x_hi and s0 % 2 == 0
+        return "first", (d, s0 - 256, neg0)
+    assert s0 == 256 + d and not neg0, "v_pk_add_f32 must accumulate in place"
+    if x_lo <= s1 - 256 < x_hi:
+        assert (tmp if G.B else acc) and s1 % 2 == 0
+        return "add", (d, s1 - 256, neg1)
+    assert G.B and acc and not neg1 and G.tmp0 <= s1 - 256 < G.tmp0 + G.nw
+    return "flush", (d, s1 - 256)
 
 
 def _decode(code, pc, G):
@@ -75,13 +108,9 @@ def _decode(code, pc, G):
     if w0 == 0xDDF48000:
         assert (w1 >> 16) == 84
         return "glds", (w1 & 0xFF,), 2
-    if (w0 & 0xFFFFFD00) == 0xD3B24000:  # v_pk_add_f32
-        d, neg = w0 & 0xFF, bool(w0 & 0x200)
-        src0, src1 = (w1 & 0x1FF) - 256, ((w1 >> 9) & 0x1FF) - 256
-        assert (w1 >> 18) & 0x1FF == 0 and (w1 >> 27) & 3 == 3 and (w1 >> 29) == (2 if neg else 0)
-        assert src0 == d, "v_pk_add_f32 must accumulate in place"
-        assert G.acc0 <= d < G.acc0 + 2 * G.nw and d % 2 == 0 and 8 <= src1 < G.lds_v and src1 % 2 == 0
-        return "add", (d, src1, neg), 2
+    if (w0 & 0xFFFFFC00) == 0xD3B24000:  # v_pk_add_f32
+        kind, f = _classify_pk(w0, w1, G)
+        return kind, f, 2
     if (w0 & 0xFFFF0000) == 0xD8EC0000:  # ds_read_b64
         assert (w1 >> 8) & 0xFFFF == 0
         return "read", (w1 >> 24, w1 & 0xFF, w0 & 0xFFFF), 2
@@ -101,6 +130,8 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
     last_read = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)
     S = G.streams
     waves = [Wave(w, int(wcode[t * S + w % S]) // 4) for w in range(WAVES)]
+    for wv in waves:
+        wv.v[G.acc0:G.acc0 + 2 * NW] = 0.0
     for wv in waves:
         assert int(wcode[t * S + wv.w % S]) % 256 == 0
     phase = 0
@@ -158,7 +189,7 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                     assert vd not in wv.reads, "X slot reloaded before its previous read was waited for"
                     wv.reads.append(vd)
                     assert G.lds_v <= a < G.lds_v + 3 and off % ROW_BYTES == 0 and off // ROW_BYTES < CHUNK
-                    assert 8 <= vd < G.lds_v
+                    assert 8 <= vd < 8 + 2 * G.xslots
                     row = (a - G.lds_v) * CHUNK + off // ROW_BYTES
                     assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
                     last_read[row] = max(last_read[row], phase)
@@ -169,6 +200,15 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                     d, x, neg = f
                     assert x not in wv.reads, "add reads an X slot whose LDS read may not have returned"
                     wv.v[d:d + 2] = wv.v[d:d + 2] - wv.v[x:x + 2] if neg else wv.v[d:d + 2] + wv.v[x:x + 2]
+                elif kind == "first":
+                    d, x, neg = f
+                    assert x not in wv.reads, "add reads an X slot whose LDS read may not have returned"
+                    xv = -wv.v[x:x + 2] if neg else wv.v[x:x + 2]
+                    wv.v[d:d + 2] = xv + np.float32(0.0)
+                elif kind == "flush":
+                    d, t = f
+                    wv.v[d:d + 2] = wv.v[d:d + 2] + wv.v[t:t + 2]
+                    wv.v[t:t + 2] = np.nan  # a block sum is consumed once
         assert at_barrier in (0, WAVES), "waves disagree on the barrier count"
         phase += 1
     acc = np.zeros((TILE_M, G.tile_cols), np.float32)
@@ -231,3 +271,72 @@ def test_jit_code_dense_and_empty_columns(tsg, oracle_mod):
     W[1::2, 2] = -1
     W[:, 5:] = O.gen_ternary(K, N - 5, 2, 3)
     _check(tsg, O, M, K, N, 0, 4, True, W=W)
+
+
+def _count_entry_adds(code, G):
+    """v_pk_add_f32 that apply one nonzero (add / first); flushes excluded."""
+    n = 0
+    for i in range(0, len(code) - 1, 2):  # every v_pk_add_f32 is 8-byte aligned
+        w0 = int(code[i])
+        if (w0 & 0xFFFFFC00) == 0xD3B24000 and (int(code[i + 1]) >> 27) & 3 == 3:
+            n += _classify_pk(w0, int(code[i + 1]), G)[0] in ("add", "first")
+    return n
+
+
+def _check_blocked(tsg, O, M, K, N, s, B, seed, frac, W=None):
+    W = O.gen_ternary(K, N, s, seed) if W is None else W
+    blk = O.blocked_tcsc_encode(W, B)
+    code, wcode = tsg.jit_codegen(*blk, K, N, B=B)
+    G = Geom(code)
+    assert G.B == B
+    X = O.init_x_frac(M, K, seed + 1) if frac else O.init_x_int(M, K, seed + 1)
+    b = np.linspace(-2, 3, N).astype(np.float32)
+    Y = emulate(code, wcode, X, K, N) + b
+    ref = O.base_blocked_tcsc(X, blk, b, K, N, B)
+    assert np.array_equal(Y.view(np.uint32), ref.view(np.uint32)), (M, K, N, s, B, frac)
+    assert _count_entry_adds(code, G) == len(blk[2]) + len(blk[3])
+
+
+@pytest.mark.parametrize("M,K,N,s,B", [(5, 70, 33, 2, 16), (130, 200, 520, 4, 64), (17, 300, 64, 8, 100),
+                                       (3, 1100, 9, 4, 512), (9, 96, 70, 2, 1), (4, 10, 5, 2, 32)])
+def test_jit_code_emulates_base_blocked_tcsc(tsg, oracle_mod, M, K, N, s, B):
+    """BaseBlockedTCSC (comp.h:607-658): y per block = 0 + pos - neg, Y += y
+    block by block, + b; blocks straddling chunks, K not a multiple of B (the
+    tail rows are not in the format), B = 1, K < B (no blocks: Y = b)."""
+    for frac in (False, True):
+        _check_blocked(tsg, oracle_mod, M, K, N, s, B, 7 + K + B, frac)
+
+
+def test_jit_code_blocked_kat(tsg, oracle_mod):
+    """The 4x4, B = 2 example of plots/data_example_image/blocked.py:12-30."""
+    import json
+    import os
+    kat = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kat_blocked_4x4_B2.json")))
+    W = np.array(kat["W"], np.int32)
+    _check_blocked(tsg, oracle_mod, 4, 4, 4, 0, 2, 1, True, W=W)
+
+
+def test_jit_code_base_unchanged_by_block_support(tsg, oracle_mod):
+    """B = 0 through the blocked entry point is the BaseTCSC code, word for word."""
+    O = oracle_mod
+    W = O.gen_ternary(200, 130, 4, 5)
+    t = O.tcsc_encode(W)
+    c0, w0 = tsg.jit_codegen(*t.arrays, 200, 130)
+    c1, w1 = tsg.jit_codegen(*t.arrays, 200, 130, B=0)
+    assert np.array_equal(c0, c1) and np.array_equal(w0, w1)
+    assert int(c0[5]) == 0
+
+
+def test_blocked_validation_rejects_malformed(tsg, oracle_mod):
+    O = oracle_mod
+    W = O.gen_ternary(64, 6, 2, 9)
+    csp, csn, rip, rin = O.blocked_tcsc_encode(W, 16)
+    tsg.validate_blocked(csp, csn, rip, rin, 64, 6, 16)
+    bad = rip.copy()
+    j = int(csp[6])  # first +1 row of block 1 (slot N) moved into block 0
+    if j < int(csp[7]):
+        bad[j] = 3
+        with pytest.raises(tsg.TSGError, match="out of its block"):
+            tsg.validate_blocked(csp, csn, bad, rin, 64, 6, 16)
+    with pytest.raises(tsg.TSGError):
+        tsg.validate_blocked(csp, csn, rip, rin, 64, 6, 0)
