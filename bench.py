@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--s", type=int, default=4)
     ap.add_argument("--seed-w", type=int, default=42)
     ap.add_argument("--seed-x", type=int, default=12345)
-    ap.add_argument("--cpu-rows", type=int, default=1024,
+    ap.add_argument("--cpu-rows", type=int, default=2048,
                     help="rows of the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--allgather", action="store_true")
     return ap.parse_args()
@@ -134,6 +134,22 @@ def main():
         allgather_ms = (time.perf_counter() - t1) / 3 * 1e3
         del Yall
 
+    # --- end to end through the comp_func surface (host pointers: H2D X, the
+    # step, D2H Y; synchronous, as the reference calls it, main.cpp:214-216).
+    # PCIe-inclusive, reported beside the headline, never as `value`.
+    e2e = None
+    if rank == 0 and world == 1:
+        Xh, bh = X.cpu().numpy(), b.cpu().numpy()
+        Yh = np.empty((M, Nr), np.float32)
+        h(Xh, bh, Yh, M, Nr, K)
+        reps = 3
+        e0 = time.perf_counter()
+        for _ in range(reps):
+            h(Xh, bh, Yh, M, Nr, K)
+        e_ms = (time.perf_counter() - e0) / reps * 1e3
+        e2e = {"ms": round(e_ms, 3), "gflops": round(T.flops(M, Nr, nnz) / (e_ms * 1e-3) / 1e9, 1),
+               "bytes_over_pcie": 4 * (M * K + Nr + M * Nr)}
+
     # --- CPU baseline: the oracle (BaseTCSC restatement, 1 thread) on a
     # bounded sample of the same workload; rank 0 at N=1 only.
     cpu = None
@@ -200,6 +216,7 @@ def main():
                                      "frac": round(adds / (kern_ms_max * 1e-3) / 1e12 / VALU_PEAK_TADDS, 4)}},
             "cpu_baseline": cpu,
             "stream_ms_per_step": round(stream_ms / a.steps, 4),
+            "e2e_host_pointers": e2e,
             "allgather_ms": None if allgather_ms is None else round(allgather_ms, 3),
             "setup_s": round(setup_s, 2),
         }

@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """BASELINE configs[3]: M=4096 K=4096 N=16384, sparsity s in {2,4,8,16}, TCSC vs
-"CSC + packed values" (readme.md:111) as the registration format.  One GPU.
+"CSC + packed values" (readme.md:111) vs BlockedTCSC<B> (BlockedTCSC.h, B=512 as
+main.cpp:7) as the registration format.  One GPU.
 
-Both formats register the same matrix (the packed one is converted on the host,
-tsg_csc_packed_to_tcsc) and run the same device kernel, so the comparison is
-format bytes and registration time; the kernel time per s is the sweep.  Every
-line also checks 8 sampled rows bit for bit against the CPU oracle.
+TCSC and CSC+packed register the same matrix (the packed one is converted on the
+host, tsg_csc_packed_to_tcsc) and run the same generated code, so that
+comparison is format bytes and registration time.  BlockedTCSC computes
+BaseBlockedTCSC (its own accumulation order, comp.h:607-658) on the same
+kernel with per-block sums.  Every line also checks 8 sampled rows bit for bit
+against the CPU oracle of its order.
 Writes one JSON object per s to stdout.
 
     python scripts/sweep.py [--steps 10]
@@ -29,6 +32,7 @@ def main():
     ap.add_argument("--M", type=int, default=4096)
     ap.add_argument("--K", type=int, default=4096)
     ap.add_argument("--N", type=int, default=16384)
+    ap.add_argument("--B", type=int, default=512, help="BlockedTCSC block size (main.cpp:7)")
     a = ap.parse_args()
     import torch
     import oracle as O
@@ -47,10 +51,14 @@ def main():
         out = {"s": s, "M": M, "K": K, "N": N, "nnz": nnz,
                "tcsc_bytes": 4 * (2 * (N + 1) + nnz),
                "csc_packed_bytes": 4 * (N + 1) + 4 * len(row_idx) + len(packed)}
-        for fmt in ("tcsc", "csc_packed"):
+        blk = T.tcsc_to_blocked(*arrs, K, N, a.B)
+        out["blocked_B"] = a.B
+        out["blocked_bytes"] = 4 * (len(blk[0]) + len(blk[1]) + len(blk[2]) + len(blk[3]))
+        for fmt in ("tcsc", "csc_packed", "blocked"):
             t0 = time.time()
             h = (T.TCSCDevice(*arrs, K, N, device=0) if fmt == "tcsc"
-                 else T.TCSCDevice.from_csc_packed(col_ptr, row_idx, packed, K, N, device=0))
+                 else T.TCSCDevice.from_csc_packed(col_ptr, row_idx, packed, K, N, device=0) if fmt == "csc_packed"
+                 else T.TCSCDevice.from_blocked(*blk, K, N, a.B, device=0))
             out[f"{fmt}_register_s"] = round(time.time() - t0, 3)
             h.reserve(M)
             for _ in range(2):
@@ -64,7 +72,9 @@ def main():
             ms, n = h.kernel_time(reset=True)
             h.set_timing(False)
             ms /= max(n, 1)
-            ref = O.base_tcsc(Xs, O.TCSC(*arrs, K, N), np.full(N, 2.0, np.float32))
+            bb = np.full(N, 2.0, np.float32)
+            ref = (O.base_blocked_tcsc(Xs, blk, bb, K, N, a.B) if fmt == "blocked"
+                   else O.base_tcsc(Xs, O.TCSC(*arrs, K, N), bb))
             out[f"{fmt}_kernel_ms"] = round(ms, 4)
             out[f"{fmt}_bit_identical_rows"] = bool(np.array_equal(ref.view(np.uint32),
                                                                    Y[:8].cpu().numpy().view(np.uint32)))

@@ -347,14 +347,20 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     // stream offsets are 32-bit, so a W whose image would pass ~3 GiB (e.g.
     // K=16384, N=131072, s=4 on ONE GPU -- shard columns instead)
     // defaults to the rx kernel.  Asking for jit explicitly is then an error.
-    const double jit_est = 8.0 * 1.25 * ((double)h->nnz_pos + (double)h->nnz_neg);
+    // A stream step (DMA, barrier, waits) costs ~256 B on top; BlockedTCSC walks
+    // every block's chunks twice per column half.
+    const int64_t nchk = std::max(1, (K + tsg::kJitChunk - 1) / tsg::kJitChunk);
+    const int64_t steps = B ? 4 * (int64_t)(K / B) * ((B + tsg::kJitChunk - 1) / tsg::kJitChunk + 1) : 2 * nchk;
+    const int64_t streams = (int64_t)((N + tsg::kJitTileCols - 1) / tsg::kJitTileCols) * tsg::kJitStreams;
+    const double jit_est =
+        8.0 * 1.25 * ((double)h->nnz_pos + (double)h->nnz_neg) + 256.0 * (double)steps * (double)streams;
     const bool jit_fits = jit_est < 3.0 * (double)(1ull << 30);
     const std::string kname = kenv ? kenv : (jit_fits ? "jit" : "rx");
-    if (B && kname != "jit") {
+    if (B && kname != "jit" && kenv) {
         delete h;
         return fail(TSG_ERR_ARG, "BlockedTCSC runs on the jit kernel only (TSG_KERNEL=" + kname + ")");
     }
-    if (kname == "jit" && !jit_fits) {
+    if ((kname == "jit" || B) && !jit_fits) {
         delete h;
         return fail(TSG_ERR_ARG, "TSG_KERNEL=jit: W has too many nonzeros for one weight-compiled image "
                                  "(> ~300M); shard columns across handles or use TSG_KERNEL=rx");

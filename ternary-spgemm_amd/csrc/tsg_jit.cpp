@@ -202,11 +202,12 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     Emit E{code};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
-    // prefetch), nolgkm (no LDS waits), noreads (no X reads)
+    // prefetch), nolgkm (no LDS waits), noreads (no X reads), halfreads (every
+    // other X read: the instruction count of 2-row reads)
     const std::string diag = std::getenv("TSG_JIT_DIAG") ? std::getenv("TSG_JIT_DIAG") : "";
     auto has = [&](const char *f) { return diag.find(f) != std::string::npos; };
     const bool d_nobar = has("nobar"), d_nodma = has("nodma"), d_notouch = has("notouch"),
-               d_nolgkm = has("nolgkm"), d_noreads = has("noreads");
+               d_nolgkm = has("nolgkm"), d_noreads = has("noreads"), d_halfreads = has("halfreads");
     // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,2)
     uint32_t touch_first = 1, touch_count = 2;
     if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
@@ -310,7 +311,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     while (rq + 1 <= qmax && issued >= first[rq + 1]) rq++;
                     if (issued >= first[rq + 1]) return;  // past step qmax
                     const int r = secs[rq].rows[(size_t)(issued - first[rq])];
-                    if (!d_noreads)
+                    if (!d_noreads && !(d_halfreads && (issued & 1)))
                         E.ds_read_b64(kXSlot0 + 2u * (uint32_t)(issued % S), kLdsBaseV + (uint32_t)(rq % 3),
                                       (uint32_t)r * kRowBytes);
                 }

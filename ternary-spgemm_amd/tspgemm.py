@@ -229,6 +229,24 @@ def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0):
     return code, wcode
 
 
+def tcsc_to_blocked(csp, csn, rip, rin, K: int, N: int, B: int):
+    """TCSC -> BlockedTCSC<B> arrays (the layout BlockedTCSC.h:15-41 builds from
+    the dense W): slot kb*N + n = column n's rows of block kb, K/B whole blocks,
+    rows past (K/B)*B dropped.  Vectorised host conversion (numpy)."""
+    nb = K // B
+    out = []
+    for cs, ri in ((_i32(csp), _i32(rip)), (_i32(csn), _i32(rin))):
+        col = np.repeat(np.arange(N, dtype=np.int64), np.diff(cs[: N + 1]))
+        blk = ri[: cs[N]].astype(np.int64) // B
+        keep = blk < nb
+        slot = blk[keep] * N + col[keep]
+        order = np.argsort(slot, kind="stable")  # within a slot: ascending k as in the column
+        starts = np.zeros(nb * N + 1, np.int32)
+        np.cumsum(np.bincount(slot, minlength=nb * N), out=starts[1:])
+        out.append((starts, ri[: cs[N]][keep][order].astype(np.int32)))
+    return out[0][0], out[1][0], out[0][1], out[1][1]
+
+
 def validate_blocked(csp, csn, rip, rin, K: int, N: int, B: int) -> None:
     """Raises TSGError unless the arrays are a well-formed BlockedTCSC<B>."""
     csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)

@@ -128,3 +128,17 @@ def test_csc_packed_conversions(tsg, oracle_mod):
     # a stored entry with value 0 (digit 1) is rejected
     with pytest.raises(tsg.TSGError):
         tsg.csc_packed_to_tcsc(np.array([0, 1]), np.array([0]), np.array([1], np.uint8), 1)
+
+
+@pytest.mark.parametrize("K,N,s,B", [(64, 6, 2, 16), (1100, 70, 4, 512), (300, 33, 8, 100), (10, 5, 2, 32),
+                                     (96, 9, 1, 1)])
+def test_tcsc_to_blocked_matches_blocked_ctor(tsg, oracle_mod, K, N, s, B):
+    """Host TCSC -> BlockedTCSC<B> conversion == the BlockedTCSC ctor
+    (BlockedTCSC.h:15-41, restated in the oracle) array for array."""
+    O = oracle_mod
+    W = O.gen_ternary(K, N, s, K + B)
+    got = tsg.tcsc_to_blocked(*O.tcsc_encode(W).arrays, K, N, B)
+    want = O.blocked_tcsc_encode(W, B)
+    for g, w in zip(got, want):
+        assert np.array_equal(np.asarray(g, np.int32), np.asarray(w, np.int32))
+    tsg.validate_blocked(*got, K, N, B)

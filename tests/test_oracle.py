@@ -157,3 +157,8 @@ def test_against_reference_build_directly(oracle_mod):
         X = O.init_x_int(9, K, seed)
         b = np.full(N, 2.0, np.float32)
         assert np.array_equal(O.base_tcsc(X, t, b), O.ref_gemm(X, W, b))
+    # BlockedTCSC<B> ctor, incl. K not a multiple of B (the tail rows are dropped)
+    for K, N, B in [(1100, 70, 512), (200, 33, 64), (10, 5, 4), (6, 4, 2)]:
+        W = O.ref_generate_sparse(K, N, 2, K + B)
+        for a, r in zip(O.blocked_tcsc_encode(W, B), O.ref_blocked_tcsc_encode(W, B)):
+            assert np.array_equal(a, r), (K, N, B)
