@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Kernel time of the default (weight-compiled) path on BASELINE.json's configs
+and on the small-M shapes of the reference's sweep (plots/run_benchmark.py:8-33),
+one GPU, each checked bit for bit on sampled rows against the CPU oracle.
+One JSON object per shape on stdout.
+
+    python scripts/configs.py [--steps 10]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "ternary-spgemm_amd"), os.path.join(REPO, "oracle")]
+import tspgemm as T  # noqa: E402
+
+SHAPES = [("configs[0]", 32, 1024, 4096, 4), ("configs[1]", 512, 4096, 4096, 4),
+          ("configs[2]", 4096, 4096, 16384, 4),
+          ("sweep M=1", 1, 4096, 16384, 4), ("sweep M=16", 16, 4096, 16384, 4),
+          ("sweep M=64", 64, 4096, 16384, 4), ("sweep M=256", 256, 4096, 16384, 4),
+          ("sweep M=1024", 1024, 4096, 16384, 4), ("run_benchmark (64000,16384,4096)", 8192, 16384, 4096, 4)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+    import oracle as O
+    dev = torch.device("cuda", 0)
+    for name, M, K, N, s in SHAPES:
+        arrs = T.gen_tcsc(K, N, s, 42)
+        nnz = len(arrs[2]) + len(arrs[3])
+        t0 = time.time()
+        h = T.TCSCDevice(*arrs, K, N, device=0)
+        reg_s = time.time() - t0
+        g = torch.Generator(device=dev)
+        g.manual_seed(12345)
+        X = torch.randint(-512, 513, (M, K), generator=g, device=dev, dtype=torch.int32).to(torch.float32)
+        b = torch.full((N,), 2.0, device=dev)
+        Y = torch.empty((M, N), device=dev)
+        h.reserve(M)
+        for _ in range(2):
+            h.gemm_torch(X, b, Y)
+        torch.cuda.synchronize()
+        h.set_timing(True)
+        h.kernel_time(reset=True)
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            h.gemm_torch(X, b, Y)
+        torch.cuda.synchronize()
+        step_ms = (time.perf_counter() - t1) / a.steps * 1e3
+        ms, n = h.kernel_time(reset=True)
+        ms /= max(n, 1)
+        rows = min(M, 8)
+        ref = O.base_tcsc(X[:rows].cpu().numpy(), O.TCSC(*arrs, K, N), np.full(N, 2.0, np.float32))
+        ok = bool(np.array_equal(ref.view(np.uint32), Y[:rows].cpu().numpy().view(np.uint32)))
+        adds = T.flops(M, N, nnz)
+        print(json.dumps({"shape": name, "M": M, "K": K, "N": N, "s": s, "kernel": h.kernel_name(),
+                          "kernel_ms": round(ms, 4), "step_ms": round(step_ms, 4),
+                          "gflops_kernel": round(adds / (ms * 1e-3) / 1e9, 1),
+                          "valu_frac": round(adds / (ms * 1e-3) / 78.64e12, 4),
+                          "workgroups": -(-M // 128) * -(-N // 512), "register_s": round(reg_s, 2),
+                          "bit_identical_rows": ok}), flush=True)
+        h.close()
+
+
+if __name__ == "__main__":
+    main()
