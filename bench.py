@@ -179,10 +179,12 @@ def main():
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
         traffic = None
         try:
+            # HBM bytes per launch of THIS kernel on THIS workload, from the
+            # committed rocprofv3 PMC passes (scripts/pmc_summary.py: FETCH_SIZE
+            # and WRITE_SIZE with the gfx950 corrections of MI355X_MICROARCH.md)
             pm = json.load(open(PROFILE_PMC))
-            key = f"{M}x{K}x{Nr}s{s}"
-            if pm.get("kernel") == kname:
-                traffic = pm.get("per_launch_hbm_bytes", {}).get(key)
+            if pm.get("workload") == f"{M}x{K}x{Nr}s{s}":
+                traffic = pm.get("kernels", {}).get(kname, {}).get("hbm_bytes")
         except Exception:
             pass
         out = {

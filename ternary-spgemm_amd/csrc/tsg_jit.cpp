@@ -100,6 +100,7 @@ struct Emit {
     void nop(uint32_t n = 0) { c.push_back(0xbf800000u | n); }
     void wait_lgkm(uint32_t n) { c.push_back(0xbf8cc07fu | (n << 8)); }  // s_waitcnt lgkmcnt(n), n <= 15
     void wait_vm0() { c.push_back(0xbf8c0f70u); }
+    void wait_vm(uint32_t n) { c.push_back(0xbf8c0f70u | n); }            // s_waitcnt vmcnt(n), n <= 15
     void barrier() { c.push_back(0xbf8a0000u); }
     void ret() { c.push_back(0xbe801d5eu); }         // s_setpc_b64 s[94:95]
     uint32_t pos_bytes() const { return (uint32_t)(c.size() * 4); }
@@ -208,9 +209,11 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     auto has = [&](const char *f) { return diag.find(f) != std::string::npos; };
     const bool d_nobar = has("nobar"), d_nodma = has("nodma"), d_notouch = has("notouch"),
                d_nolgkm = has("nolgkm"), d_noreads = has("noreads"), d_halfreads = has("halfreads");
-    // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,2)
-    uint32_t touch_first = 1, touch_count = 2;
+    // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,1)
+    uint32_t touch_first = 1, touch_count = 1;
     if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
+    if (touch_count > 4) touch_count = 4;
+    const uint32_t ntouch = d_notouch ? 0u : touch_count;
 
     int n0 = 0;  // first column of the current stream
     std::vector<int32_t> cur((size_t)kJitNW * 2), end((size_t)kJitNW * 2);
@@ -342,7 +345,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     }
                 };
                 if (q + 2 < steps) emit_dma(q + 2);
-                for (uint32_t d = 0; d < (d_notouch ? 0u : touch_count); d++) {
+                // code touches go out AFTER the step's DMA: VMEM loads return in
+                // order, so the step's closing vmcnt(ntouch) waits for every DMA
+                // piece but lets the touches (L2 misses) run into the next step
+                for (uint32_t d = 0; d < ntouch; d++) {
                     E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
                     E.nop(4);
                     E.code_touch(kSinkV, kLane128V);
@@ -381,9 +387,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                             live[col] = 0;
                         }
                 issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first rows
-                E.wait_vm0();
+                E.wait_vm(ntouch);
                 if (!d_nobar) E.barrier();
             }
+            E.wait_vm0();  // no load outstanding past the stream
             E.restore_m0();
             E.ret();
         }

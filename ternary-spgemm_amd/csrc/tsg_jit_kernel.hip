@@ -119,12 +119,17 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     // ids (blocks b and b+8 share an XCD), and consecutive ids walk groups of
     // kGN column tiles x kGM M tiles, so the ~32 workgroups an XCD runs at once
     // share kGN code streams and kGM X^T slabs through its L2 instead of 1 and
-    // 32 (DESIGN.md 5: traffic beyond L2 = kGN x code + kGM x slab per round).
+    // 32 (DESIGN.md 4: traffic beyond L2 = kGN x code + kGM x slab per round).
+    // Measured placement (scripts/hwid_micro.hip): an XCD's slot s goes to
+    // shader engine s % 4 (rotated), CU s / 4 of it, so nt = slot % kGN puts
+    // every CU of an SE on the same column tile: the CU pairs that share an
+    // instruction cache fetch one code stream (kGN = 8 splits them: +25%).
+    // kGN = 2 (two SEs per tile) measured 4-6% faster than 4 (profiles/r01c_ab_mapping.txt).
 #ifndef TSG_JIT_GN
-#define TSG_JIT_GN 4
+#define TSG_JIT_GN 2
 #endif
 #ifndef TSG_JIT_GM
-#define TSG_JIT_GM 8
+#define TSG_JIT_GM 16
 #endif
     constexpr int kGN = TSG_JIT_GN, kGM = TSG_JIT_GM;
     const int T = mtiles * ntiles, L = blockIdx.x;
@@ -137,7 +142,11 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const int stream = wave % kJStreams, ms = wave / kJStreams;  // column stream, 128-row M slice
     const int ncol0 = nt * kJTileCols + stream * kJNW;
 
+#ifdef TSG_JIT_SAMETILE  // diagnostic (results WRONG): every workgroup runs column tile 0's code
+    const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[stream]);
+#else
     const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJStreams + stream]);
+#endif
     const uint32_t lb0 = (uint32_t)(ms * 512 + lane * 8), lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
     // LDS-DMA piece i of this wave: chunk rows kJPieceRows*(wave*P + i) + lane / (64 / kJPieceRows)
     constexpr int kLanesPerRow = 64 / kJPieceRows;

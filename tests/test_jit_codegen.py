@@ -3,7 +3,8 @@ runs it.  tsg_jit_codegen's region is decoded instruction by instruction (only
 the gfx950 encodings the generator may emit are accepted) and a whole
 workgroup is emulated against the register contract of
 ternary-spgemm_amd/csrc/tsg_jit_kernel.hip: its 16 waves run barrier phase by
-barrier phase, LDS-DMA copies land at the issuing wave's `s_waitcnt vmcnt(0)`,
+barrier phase, LDS-DMA copies land at the issuing wave's `s_waitcnt vmcnt(n)` (VMEM loads
+return in order: all but the newest n),
 and every LDS read is checked to see data that landed in an EARLIER phase (no
 read-after-DMA race) while no DMA may overwrite rows read since it was issued
 (no write-after-read race).  Code-prefetch loads must stay inside the region.
@@ -56,7 +57,8 @@ class Wave:
         self.saved_m0 = None
         self.base = None
         self.touch = None
-        self.pending = []  # DMA copies not yet landed: (lds_byte, data, issue_phase)
+        self.pending = []  # VMEM loads not yet returned, oldest first: the DMA copies of one
+        #                    global_load_lds [(lds_byte, data, issue_phase)...] or [] (code touch)
         self.reads = []    # X slot registers of LDS reads not yet waited for, oldest first
         self.done = False
 
@@ -93,7 +95,9 @@ def _decode(code, pc, G):
         return "nop", (), 1
     if (w0 & 0xFFFFF0FF) == 0xBF8CC07F:
         return "wait_lgkm", ((w0 >> 8) & 0xF,), 1
-    simple = {0xBF8C0F70: "wait_vm", 0xBF8A0000: "barrier", 0xBED6007C: "save_m0",
+    if (w0 & 0xFFFFFFF0) == 0xBF8C0F70:  # s_waitcnt vmcnt(n), n <= 15
+        return "wait_vm", (w0 & 0xF,), 1
+    simple = {0xBF8A0000: "barrier", 0xBED6007C: "save_m0",
               0xBEFC0056: "restore_m0", 0xBED40150: "base_reset", 0xBE801D5E: "ret", 0x82558055: "base_addc",
               0x8259805D: "touch_addc", 0x80545254: "base_add"}
     if w0 in simple:
@@ -164,6 +168,7 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                     wv.touch = f[0]
                 elif kind == "touch":
                     assert wv.touch is not None and wv.touch + 63 * 128 + 4 <= region_bytes, "prefetch past region"
+                    wv.pending.append([])
                 elif kind == "glds":
                     i = f[0] - G.dma_v
                     assert 0 <= i < PIECES
@@ -171,16 +176,18 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                     j, rem = divmod(wv.base - XT_BASE, stride)
                     assert rem == 0 and 0 <= j < nch
                     assert wv.m0 % BUF_BYTES == chunk_row0 * ROW_BYTES, "DMA lands on the wrong rows"
-                    for half in range(G.piece_rows):
-                        src = XT[j * CHUNK + chunk_row0 + half, m0:m0 + TILE_M]
-                        wv.pending.append((wv.m0 + half * ROW_BYTES, src.copy(), phase))
-                elif kind == "wait_vm":
-                    for dst, data, iss in wv.pending:
-                        row = dst // ROW_BYTES
-                        assert last_read[row] < iss, "DMA overwrites a row read since its issue (WAR race)"
-                        lds[dst // 4:dst // 4 + TILE_M] = data
-                        landed[row] = phase
-                    wv.pending = []
+                    wv.pending.append([(wv.m0 + half * ROW_BYTES, XT[j * CHUNK + chunk_row0 + half,
+                                                                       m0:m0 + TILE_M].copy(), phase)
+                                       for half in range(G.piece_rows)])
+                elif kind == "wait_vm":  # loads return in order: all but the newest f[0] land
+                    n_land = max(len(wv.pending) - f[0], 0)
+                    for op in wv.pending[:n_land]:
+                        for dst, data, iss in op:
+                            row = dst // ROW_BYTES
+                            assert last_read[row] < iss, "DMA overwrites a row read since its issue (WAR race)"
+                            lds[dst // 4:dst // 4 + TILE_M] = data
+                            landed[row] = phase
+                    wv.pending = wv.pending[n_land:]
                 elif kind == "wait_lgkm":
                     while len(wv.reads) > f[0]:  # LDS returns in order
                         wv.reads.pop(0)
