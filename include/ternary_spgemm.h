@@ -110,8 +110,20 @@ int tcsc_hip_gemm_prelu(tsg_tcsc *h, const float *X, const float *b, const float
 int tcsc_hip_gemm_prelu_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha,
                             float *dY, int M, int N, int K, void *stream);
 
-/* Pre-allocates the per-handle work buffer for row counts up to max_M. */
+/* Pre-allocates the per-handle work buffer for row counts up to max_M and, on
+ * the weight-compiled kernel, compiles the code image a call with max_M rows
+ * runs (tcsc_hip_jit_width), so no later call compiles (graph capture). */
 int tcsc_hip_reserve(tsg_tcsc *h, int max_M);
+
+/* Weight-compiled kernel: columns per generated stream (a wave's columns).
+ * 64 is the default; small-M calls use narrower streams (32, 16, 8) so more
+ * workgroups fill the GPU -- each width is its own code image, compiled on the
+ * first call (or tcsc_hip_reserve) that picks it.  Same results bit for bit.
+ * tcsc_hip_jit_width: the width a call with M rows runs (0: not a jit handle).
+ * tcsc_hip_set_jit_width: 0 = automatic (default), or pin 64/32/16/8
+ * (BlockedTCSC: 64 only).  Extension: no reference counterpart. */
+int tcsc_hip_jit_width(const tsg_tcsc *h, int M);
+int tcsc_hip_set_jit_width(tsg_tcsc *h, int width);
 
 /* ---- introspection ------------------------------------------------------- */
 typedef struct tsg_info {
@@ -193,6 +205,12 @@ int tsg_jit_codegen_blocked(const int32_t *col_start_pos, const int32_t *col_sta
                             const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
                             int B, uint32_t *code, int64_t code_cap, int64_t *code_len,
                             uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+
+/* Same with an explicit stream width (64, 32, 16, 8; BlockedTCSC: 64). */
+int tsg_jit_codegen_w(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                      const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                      int B, int width, uint32_t *code, int64_t code_cap, int64_t *code_len,
+                      uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
 
 /* Checks BlockedTCSC<B> arrays (layout as tcsc_hip_create_blocked): monotone
  * column starts, every row inside its block, ascending, no row both +1 and -1. */

@@ -4,7 +4,10 @@ and on the small-M shapes of the reference's sweep (plots/run_benchmark.py:8-33)
 one GPU, each checked bit for bit on sampled rows against the CPU oracle.
 One JSON object per shape on stdout.
 
-    python scripts/configs.py [--steps 10]
+    python scripts/configs.py [--steps 10] [--all-widths]
+
+--all-widths times every jit stream width (64/32/16/8) per shape, besides the
+automatic pick, to check tsg_capi.cpp pick_jit_width.
 """
 import argparse
 import json
@@ -28,15 +31,23 @@ SHAPES = [("configs[0]", 32, 1024, 4096, 4), ("configs[1]", 512, 4096, 4096, 4),
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--all-widths", action="store_true")
+    ap.add_argument("--only", default="", help="substring filter on shape names")
     a = ap.parse_args()
     import torch
     import oracle as O
     dev = torch.device("cuda", 0)
     for name, M, K, N, s in SHAPES:
+      if a.only and a.only not in name:
+          continue
+      for width in ([0, 64, 32, 16, 8] if a.all_widths else [0]):
         arrs = T.gen_tcsc(K, N, s, 42)
         nnz = len(arrs[2]) + len(arrs[3])
         t0 = time.time()
         h = T.TCSCDevice(*arrs, K, N, device=0)
+        if width:
+            h.set_jit_width(width)
+        jw = h.jit_width(M)
         reg_s = time.time() - t0
         g = torch.Generator(device=dev)
         g.manual_seed(12345)
@@ -64,7 +75,8 @@ def main():
                           "kernel_ms": round(ms, 4), "step_ms": round(step_ms, 4),
                           "gflops_kernel": round(adds / (ms * 1e-3) / 1e9, 1),
                           "valu_frac": round(adds / (ms * 1e-3) / 78.64e12, 4),
-                          "workgroups": -(-M // 128) * -(-N // 512), "register_s": round(reg_s, 2),
+                          "jit_width": jw, "width_pinned": bool(width),
+                          "workgroups": -(-M // 128) * -(-N // (8 * max(jw, 1))), "register_s": round(reg_s, 2),
                           "bit_identical_rows": ok}), flush=True)
         h.close()
 

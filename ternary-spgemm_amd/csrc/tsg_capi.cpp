@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -39,11 +40,20 @@ struct tsg_tcsc {
     tsg::Image img;                       // v1 device image (chunked kernel)
     tsg::StreamImage simg;                // device image of the stream kernel
     tsg::RxImage rimg;                    // device image of the rx kernel
-    tsg::JitImage jimg;                   // generated code of the jit kernel (code freed once loaded)
-    tsg::JitModule jmod;                  // dispatcher + generated code, loaded
+    // jit kernel: one compiled image per stream width (index tsg::kJitWidths):
+    // the default width at registration, narrower ones on the first call with
+    // an M that picks them (or tcsc_hip_reserve)
+    struct JitVariant {
+        int nw = 0, Npad = 0;
+        tsg::JitModule mod;               // dispatcher + generated code, loaded
+        uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
+        bool checked = false;             // status read back once after the first launch
+        int64_t code_bytes = 0, wcode_words = 0;
+    };
+    JitVariant jv[4];
+    int jit_nch = 0;                      // X^T chunks (all widths)
+    int jit_force = 0;                    // tcsc_hip_set_jit_width / TSG_JIT_NW: 0 = auto
     uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
-    bool jit_checked = false;             // status read back once after the first launch
-    int64_t jit_code_bytes = 0;
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
@@ -93,7 +103,7 @@ int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp)
 {
     const int tm = h->kind == tsg_tcsc::kRx ? tsg::kRxTileM : h->kind == tsg_tcsc::kJit ? tsg::kJitTileM : tsg::kTileM;
     Mp = ((std::max(M, 1) + tm - 1) / tm) * tm;
-    Kp = h->kind == tsg_tcsc::kJit      ? h->jimg.nch * tsg::kJitChunk
+    Kp = h->kind == tsg_tcsc::kJit      ? h->jit_nch * tsg::kJitChunk
          : h->kind == tsg_tcsc::kRx     ? h->rimg.nch * tsg::kRxChunk
          : h->kind == tsg_tcsc::kStream ? h->simg.nch * tsg::kSChunk
                                         : h->img.nch * tsg::kChunkK;
@@ -142,6 +152,93 @@ int ensure_events(tsg_tcsc *h)
     return TSG_OK;
 }
 
+int width_index(int nw)
+{
+    for (int i = 0; i < 4; i++)
+        if (tsg::kJitWidths[i] == nw) return i;
+    return -1;
+}
+
+// Stream width for a call with M rows (DESIGN.md 4 "Small M").  A workgroup is
+// one 128-row M tile x 8 streams of nw columns; it walks every X^T chunk once
+// per pass.  Per step and workgroup the adds cost 8 * nw * 96 * d * 4 / 4
+// VALU cycles at ~65% issue efficiency (d: nonzeros per pass per entry) and
+// the X-row reads 8 * 96 * (1 - (1 - d)^nw) * 512 B of LDS at 128 B/clk; a
+// launch is ceil(workgroups / 256 CUs) rounds of 2 * nch steps.  Narrow
+// streams win when the default width leaves CUs idle (config 2: 32 of 256).
+int pick_jit_width(const tsg_tcsc *h, int M)
+{
+    if (h->B) return tsg::kJitNW;
+    if (h->jit_force) return h->jit_force;
+    const double KN = std::max(1.0, (double)h->K * (double)h->N);
+    const double mt = (double)((std::max(M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM);
+    int best = tsg::kJitNW;
+    double best_t = 0;
+    for (int nw : tsg::kJitWidths) {
+        if (!tsg::jit_width_ok(nw)) continue;
+        const double ntile = (double)((h->N + 8 * nw - 1) / (8 * nw)), tiles = mt * ntile;
+        const double rounds = std::ceil(tiles / 256.0);
+        double t = 0, image = 8.0 * (double)(h->nnz_pos + h->nnz_neg);
+        for (const int64_t nnz : {h->nnz_pos, h->nnz_neg}) {
+            const double d = (double)nnz / KN, rows = tsg::kJitChunk * (1.0 - std::pow(1.0 - d, nw));
+            const double valu = 8.0 * nw * tsg::kJitChunk * d / 0.65;
+            const double lds = 8.0 * rows * 512.0 / 128.0;
+            t += (std::max(valu, lds) + 300.0) * h->jit_nch;
+            image += ntile * 8.0 * h->jit_nch * (160.0 + 8.0 * rows);  // reads + step scaffolding
+        }
+        t *= rounds;
+        if (nw != tsg::kJitNW && image > 2.0 * (double)(1ull << 30)) continue;  // 32-bit stream offsets
+        if (best_t == 0 || t < 0.97 * best_t) {
+            best = nw;
+            best_t = t;
+        }
+    }
+    return best;
+}
+
+// Compiles and loads the image of one stream width (registration, or the first
+// call that picks the width).  Caller holds h->mu (or owns h exclusively).
+int ensure_jit_variant(tsg_tcsc *h, int nw)
+{
+    const int i = width_index(nw);
+    if (i < 0 || !tsg::jit_width_ok(nw)) return fail(TSG_ERR_ARG, "unsupported jit stream width " + std::to_string(nw));
+    tsg_tcsc::JitVariant &v = h->jv[i];
+    if (v.mod.function) return TSG_OK;
+    tsg::JitImage img;
+    tsg::build_jit_code(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
+                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw);
+    if (nw == tsg::kJitNW)
+        if (const char *d = std::getenv("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
+            const size_t S = tsg::kJitStreams;
+            if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
+                for (size_t k = S; k < img.wcode.size(); k++) img.wcode[k] = img.wcode[k % S];
+            if (std::strstr(d, "samewave"))  // every wave of a tile runs its wave 0's stream
+                for (size_t k = 0; k < img.wcode.size(); k++) img.wcode[k] = img.wcode[k - k % S];
+            if (std::strstr(d, "pairwave"))  // waves 2i and 2i+1 share a stream
+                for (size_t k = 0; k < img.wcode.size(); k++) img.wcode[k] = img.wcode[k & ~(size_t)1];
+        }
+    DeviceGuard g(h->device);
+    const std::string err = v.mod.load(img.code, nw);
+    if (!err.empty()) return fail(TSG_ERR_HIP, "jit kernel (width " + std::to_string(nw) + "): " + err);
+    const size_t wb = img.wcode.size() * sizeof(uint32_t);
+    if (hipMalloc(&v.d_wcode, std::max<size_t>(wb, 4)) != hipSuccess) {
+        v.mod.unload();
+        return fail(TSG_ERR_NOMEM, "hipMalloc of the jit stream table failed");
+    }
+    if (hipMemcpy(v.d_wcode, img.wcode.data(), wb, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(v.d_wcode);
+        v.d_wcode = nullptr;
+        v.mod.unload();
+        return fail(TSG_ERR_HIP, "upload of the jit stream table failed");
+    }
+    v.nw = nw;
+    v.Npad = img.Npad;
+    v.code_bytes = (int64_t)img.code.size() * 4;
+    v.wcode_words = (int64_t)img.wcode.size();
+    h->jit_nch = img.nch;
+    return TSG_OK;
+}
+
 int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, float *dY, int M,
             int N, int K, hipStream_t s, bool prelu)
 {
@@ -159,10 +256,18 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     if (rc) return rc;
     int Mp, Kp;
     dims_for(h, M, Mp, Kp);
+    tsg_tcsc::JitVariant *jv = nullptr;
     if (h->kind == tsg_tcsc::kJit) {
+        const int nw = pick_jit_width(h, M);
+        {
+            std::lock_guard<std::mutex> lk(h->mu);
+            rc = ensure_jit_variant(h, nw);
+        }
+        if (rc) return rc;
+        jv = &h->jv[width_index(nw)];
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
-        const int64_t wgs = (int64_t)(Mp / tsg::kJitTileM) * (h->jimg.Npad / tsg::kJitTileCols);
+        const int64_t wgs = (int64_t)(Mp / tsg::kJitTileM) * (jv->Npad / (jv->nw * tsg::kJitStreams));
         if ((int64_t)Mp * tsg::kJitChunk * 4 >= (1ll << 31) || wgs * tsg::kJitWaves * 64 >= (1ll << 32))
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " is too large for one jit launch; split the rows");
     }
@@ -189,8 +294,8 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         HIP_TRY(hipMalloc(&stamps, nstamp * 8));
     }
     const int lrc = h->kind == tsg_tcsc::kJit
-        ? tsg::launch_tcsc_jit(h->jmod, h->d_work, Mp, h->d_seg, db, dalpha, dY, M, N, h->jimg.Npad,
-                               h->jimg.nch, prelu ? 1 : 0, h->d_status, s)
+        ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
+                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * tsg::kJitStreams, s)
         : h->kind == tsg_tcsc::kRx
         ? tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, stamps, s)
@@ -220,13 +325,13 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
                      nw, tot / nw, work / nw, 100 * work / tot, wait / nw, 100 * wait / tot, wmax,
                      2 * (h->kind == tsg_tcsc::kRx ? h->rimg.nch : h->simg.nch));
     }
-    if (h->kind == tsg_tcsc::kJit && !h->jit_checked) {
+    if (jv && !jv->checked) {
         // one-time check that the dispatcher found the generated region
         uint32_t st = 0;
         HIP_TRY(hipMemcpyAsync(&st, h->d_status, sizeof st, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (st != 0) return fail(TSG_ERR_HIP, "jit kernel: generated code region not found (status " + std::to_string(st) + ")");
-        h->jit_checked = true;
+        jv->checked = true;
     }
     if (slot >= 0) {
         HIP_TRY(hipEventRecord(h->ev1[slot], s));
@@ -280,7 +385,10 @@ void free_handle(tsg_tcsc *h)
     for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_zero, (void *)h->d_x,
                     (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha, (void *)h->d_status})
         if (p) (void)hipFree(p);
-    h->jmod.unload();
+    for (auto &v : h->jv) {
+        if (v.d_wcode) (void)hipFree(v.d_wcode);
+        v.mod.unload();
+    }
     if (h->stream) (void)hipStreamDestroy(h->stream);
     for (int i = 0; i < tsg_tcsc::kRing; i++) {
         if (h->ev0[i]) (void)hipEventDestroy(h->ev0[i]);
@@ -377,26 +485,21 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     const std::vector<uint32_t> *segv, *entv;
     static const std::vector<uint32_t> kNoEntries(1, 0u);
     if (h->kind == tsg_tcsc::kJit) {
-        tsg::build_jit_code(csp, csn, rip, rin, K, N, B, h->jimg);
-        h->jit_code_bytes = (int64_t)h->jimg.code.size() * 4;
-        DeviceGuard g0(device);
-        const std::string err = h->jmod.load(h->jimg.code);
-        std::vector<uint32_t>().swap(h->jimg.code);  // the loader holds its own copy
-        if (!err.empty()) {
+        // TSG_JIT_NW=<64|32|16|8> pins the stream width (A/B); default: per call
+        if (const char *wv = std::getenv("TSG_JIT_NW")) {
+            const int nw = std::atoi(wv);
+            if (width_index(nw) < 0 || !tsg::jit_width_ok(nw) || (B && nw != tsg::kJitNW)) {
+                free_handle(h);
+                return fail(TSG_ERR_ARG, std::string("TSG_JIT_NW=") + wv + ": expected 64, 32, 16 or 8 (64 for BlockedTCSC)");
+            }
+            h->jit_force = nw;
+        }
+        const int rc0 = ensure_jit_variant(h, h->jit_force ? h->jit_force : tsg::kJitNW);
+        if (rc0) {
             free_handle(h);
-            return fail(TSG_ERR_HIP, "jit kernel: " + err);
+            return rc0;
         }
-        if (const char *d = std::getenv("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
-            if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
-                for (size_t i = tsg::kJitStreams; i < h->jimg.wcode.size(); i++)
-                    h->jimg.wcode[i] = h->jimg.wcode[i % tsg::kJitStreams];
-            if (std::strstr(d, "samewave"))  // every wave of a tile runs its wave 0's stream
-                for (size_t i = 0; i < h->jimg.wcode.size(); i++)
-                    h->jimg.wcode[i] = h->jimg.wcode[i - i % tsg::kJitStreams];
-            if (std::strstr(d, "pairwave"))  // waves 2i and 2i+1 share a stream
-                for (size_t i = 0; i < h->jimg.wcode.size(); i++) h->jimg.wcode[i] = h->jimg.wcode[i & ~(size_t)1];
-        }
-        segv = &h->jimg.wcode;
+        segv = &kNoEntries;
         entv = &kNoEntries;
     } else if (h->kind == tsg_tcsc::kRx) {
         tsg::build_rx_image(csp, csn, rip, rin, K, N, h->rimg);
@@ -526,7 +629,27 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
 {
     if (!h || max_M < 0) return fail(TSG_ERR_ARG, "bad reserve arguments");
     DeviceGuard g(h->device);
-    return ensure_work(h, max_M);
+    int rc = ensure_work(h, max_M);
+    if (rc || h->kind != tsg_tcsc::kJit) return rc;
+    std::lock_guard<std::mutex> lk(h->mu);  // the image a call with max_M rows runs, compiled now
+    return ensure_jit_variant(h, pick_jit_width(h, max_M));
+}
+
+extern "C" int tcsc_hip_set_jit_width(tsg_tcsc *h, int width)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    if (h->kind != tsg_tcsc::kJit) return fail(TSG_ERR_ARG, "tcsc_hip_set_jit_width: not a jit handle");
+    if (width != 0 && (width_index(width) < 0 || !tsg::jit_width_ok(width) || (h->B && width != tsg::kJitNW)))
+        return fail(TSG_ERR_ARG, "tcsc_hip_set_jit_width: expected 0 (auto), 64, 32, 16 or 8 (64 for BlockedTCSC)");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->jit_force = width;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_jit_width(const tsg_tcsc *h, int M)
+{
+    if (!h || h->kind != tsg_tcsc::kJit) return 0;
+    return pick_jit_width(h, M);
 }
 
 extern "C" int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K)
@@ -566,7 +689,9 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     // TCSC / BlockedTCSC getDataStructureSize (TCSC.h:43-49, BlockedTCSC.h:43-47)
     o->tcsc_bytes = 4 * (2 * (int64_t)h->csp.size() + h->nnz_pos + h->nnz_neg);
     const bool rx = h->kind == tsg_tcsc::kRx || h->kind == tsg_tcsc::kJit;
-    o->image_bytes = h->kind == tsg_tcsc::kJit ? h->jit_code_bytes + (int64_t)h->jimg.wcode.size() * 4
+    int64_t jit_bytes = 0;
+    for (const auto &v : h->jv) jit_bytes += v.code_bytes + v.wcode_words * 4;
+    o->image_bytes = h->kind == tsg_tcsc::kJit ? jit_bytes
                      : rx ? (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4
                      : h->stream_kernel ? (int64_t)(h->simg.wstart.size() + h->simg.ent.size()) * 4
                                         : (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;

@@ -137,25 +137,32 @@ constexpr int kJitChunk = TSG_JIT_GEOM == 3 ? 48 : 96;
 constexpr int kJitSlots = TSG_JIT_GEOM == 2 ? 24 : 48;  // X slot registers v[8 : 8 + 2 * slots)
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
 
+// Stream width: columns per generated stream.  kJitNW (64) is the default;
+// narrower streams (32, 16, 8: same register contract, fewer accumulators,
+// dispatcher lib/tsg_jit_w<nw>.co) give small-M calls more workgroups
+// (tsg_capi.cpp pick_jit_width).  BlockedTCSC runs at kJitNW only.
+constexpr int kJitWidths[] = {kJitNW, 32, 16, 8};
+inline bool jit_width_ok(int nw) { return nw == kJitNW || (TSG_JIT_GEOM == 1 && (nw == 32 || nw == 16 || nw == 8)); }
+
 struct JitImage {
-    int K = 0, N = 0, Npad = 0, nch = 0, B = 0;
+    int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0;
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
     std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
 };
 // B = 0: BaseTCSC order (comp.h:25-69); B > 0: BaseBlockedTCSC<B> order
 // (comp.h:607-658) from BlockedTCSC<B> arrays
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                    const int32_t *rin, int K, int N, int B, JitImage &img);
+                    const int32_t *rin, int K, int N, int B, JitImage &img, int nw = kJitNW);
 
 struct JitModule {
     void *module = nullptr;        // hipModule_t
     void *function = nullptr;      // hipFunction_t of tsg_jit_kernel
-    std::string load(const std::vector<uint32_t> &code);  // "" on success
+    std::string load(const std::vector<uint32_t> &code, int nw = kJitNW);  // "" on success
     void unload();
 };
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
-                    int prelu, uint32_t *status, void *stream);
+                    int prelu, uint32_t *status, int tile_cols, void *stream);
 
 // ---------------------------------------------------------------------------
 // "chunked" kernel (tsg_tcsc_lds_kernel, round-1 v1, kept for A/B)

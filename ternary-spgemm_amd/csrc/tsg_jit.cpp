@@ -121,6 +121,7 @@ constexpr uint32_t kDmaOffV = kSinkV + 1;                  // + i: DMA piece i o
 constexpr uint32_t kLane128V = kDmaOffV + kPieces;
 constexpr uint32_t kAcc0 = (kLane128V + 2) & ~1u;         // column c: v[acc0 + 2c : acc0 + 2c + 1]
 static_assert(kAcc0 + 2 * kJitNW <= (TSG_JIT_GEOM == 2 ? 128u : 256u), "VGPR budget");
+// narrower streams (jit width < kJitNW) use the same register contract, fewer accumulators
 constexpr int kTailPad = 32768 + 1024;   // words of padding after the last stream (code prefetch reads ahead)
 static_assert((kJitChunk - 1) * kRowBytes < 65536, "ds_read offset field");
 
@@ -150,16 +151,16 @@ struct StepSpec {
 // a wave runs its columns in two halves (y of half the columns in the upper
 // X-slot registers); per half, block by block: pass 0 over the chunks the
 // block touches, pass 1, then Y += y.
-std::vector<StepSpec> plan_steps(int K, int N, int B, int nch)
+std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw)
 {
     std::vector<StepSpec> plan;
     const int C = kJitChunk;
     if (!B) {
         for (int p = 0; p < 2; p++)
-            for (int j = 0; j < nch; j++) plan.push_back({j, p, 0, kJitNW, j * C, j * C + C, 0, j == 0, false});
+            for (int j = 0; j < nch; j++) plan.push_back({j, p, 0, nw, j * C, j * C + C, 0, j == 0, false});
         return plan;
     }
-    const int nb = K / B, half = kJitNW / 2;  // rows past nb * B are not in the format (BlockedTCSC.h:17)
+    const int nb = K / B, half = nw / 2;  // rows past nb * B are not in the format (BlockedTCSC.h:17)
     for (int h = 0; h < 2; h++)
         for (int kb = 0; kb < nb; kb++) {
             const int r0 = kb * B, r1 = r0 + B, jlo = r0 / C, jhi = (r1 - 1) / C;
@@ -174,19 +175,22 @@ std::vector<StepSpec> plan_steps(int K, int N, int B, int nch)
 }  // namespace
 
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
-                    int K, int N, int B, JitImage &img)
+                    int K, int N, int B, JitImage &img, int nw)
 {
+    if (nw <= 0) nw = kJitNW;
+    const int tile_cols = nw * kJitStreams;
     img.K = K;
     img.N = N;
     img.B = B;
-    img.Npad = ((N + kJitTileCols - 1) / kJitTileCols) * kJitTileCols;
+    img.nw = nw;
+    img.Npad = ((N + tile_cols - 1) / tile_cols) * tile_cols;
     img.nch = std::max(1, (K + kJitChunk - 1) / kJitChunk);
-    const int nch = img.nch, ntiles = img.Npad / kJitTileCols;
-    const std::vector<StepSpec> plan = plan_steps(K, N, B, nch);
+    const int nch = img.nch, ntiles = img.Npad / tile_cols;
+    const std::vector<StepSpec> plan = plan_steps(K, N, B, nch, nw);
     const int steps = (int)plan.size();
     // X slots: all of v[8 : lds) for BaseTCSC; BlockedTCSC keeps y of half the
-    // columns (kJitNW registers) at the top of that range
-    const int S = B ? kJitSlots - kJitNW / 2 : kJitSlots;
+    // columns (nw registers) at the top of that range
+    const int S = B ? kJitSlots - nw / 2 : kJitSlots;
     const uint32_t kTmp0 = kXSlot0 + 2u * (uint32_t)S;  // y of column c0 + c: v[tmp0 + 2c : +1]
     img.wcode.assign((size_t)ntiles * kJitStreams, 0u);
     std::vector<uint32_t> &code = img.code;
@@ -197,7 +201,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // header: magic, then the geometry (tests/test_jit_codegen.py derives the
     // register contract from it), the block size and the X slots in use
     code.insert(code.end(), {kJitMagic0, kJitMagic1,
-                             (uint32_t)kJitWaves | (uint32_t)kJitNW << 8 | (uint32_t)kJitChunk << 16,
+                             (uint32_t)kJitWaves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
                              (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S, 0u});
     Emit E{code};
@@ -216,8 +220,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     const uint32_t ntouch = d_notouch ? 0u : touch_count;
 
     int n0 = 0;  // first column of the current stream
-    std::vector<int32_t> cur((size_t)kJitNW * 2), end((size_t)kJitNW * 2);
-    std::vector<uint8_t> live(kJitNW, 0);  // BlockedTCSC: y of the column holds an entry
+    std::vector<int32_t> cur((size_t)nw * 2), end((size_t)nw * 2);
+    std::vector<uint8_t> live(nw, 0);  // BlockedTCSC: y of the column holds an entry
     // step q's section: consumes the wave's entries in rows [klo, khi) of its pass
     auto build_section = [&](int q, Section &sec) {
         const StepSpec &sp = plan[(size_t)q];
@@ -284,7 +288,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         for (int w = 0; w < kJitStreams; w++) {
             while (code.size() % 64) E.nop();  // 256-B aligned stream start
             img.wcode[(size_t)t * kJitStreams + w] = E.pos_bytes();
-            n0 = t * kJitTileCols + w * kJitNW;
+            n0 = t * tile_cols + w * nw;
             std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
             E.save_m0();
@@ -368,7 +372,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         }
                     } else {
                         // per column its entries of the group; columns in pairs, interleaved
-                        std::vector<std::vector<uint32_t>> xs(kJitNW);
+                        std::vector<std::vector<uint32_t>> xs(nw);
                         for (int i = i0; i < i1; i++) {
                             const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % S);
                             for (uint8_t col : sec.cols[i]) xs[col].push_back(x);
@@ -401,22 +405,25 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
 // ------------------------------------------------------------ code object --
 namespace {
 
-std::string template_path()
+// The dispatcher of a stream width: lib/tsg_jit.co (kJitNW columns per wave)
+// or lib/tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile).
+std::string template_path(int nw)
 {
+    const std::string name = nw == kJitNW ? "tsg_jit.co" : "tsg_jit_w" + std::to_string(nw) + ".co";
     Dl_info info;
     if (dladdr(reinterpret_cast<void *>(&build_jit_code), &info) && info.dli_fname) {
         std::string p(info.dli_fname);
         const size_t s = p.rfind('/');
-        return (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/tsg_jit.co";
+        return (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/" + name;
     }
-    return "tsg_jit.co";
+    return name;
 }
 
 }  // namespace
 
-std::string JitModule::load(const std::vector<uint32_t> &code)
+std::string JitModule::load(const std::vector<uint32_t> &code, int nw)
 {
-    const std::string path = template_path();
+    const std::string path = template_path(nw);
     std::ifstream f(path, std::ios::binary);
     if (!f) return "cannot open jit template " + path;
     std::vector<unsigned char> img((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -494,9 +501,9 @@ void JitModule::unload()
 
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
-                    uint32_t *status, void *stream)
+                    uint32_t *status, int tile_cols, void *stream)
 {
-    int mtiles = Mp / kJitTileM, ntiles = Npad / kJitTileCols;
+    int mtiles = Mp / kJitTileM, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
                       (void *)&status};
@@ -510,11 +517,15 @@ int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t
 // ---------------------------------------------------------------- C-ABI --
 extern thread_local std::string g_tsg_host_err;
 
-extern "C" int tsg_jit_codegen_blocked(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                                       const int32_t *rin, int K, int N, int B, uint32_t *code,
-                                       int64_t code_cap, int64_t *code_len, uint32_t *wcode, int64_t wcode_cap,
-                                       int64_t *wcode_len)
+extern "C" int tsg_jit_codegen_w(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                                 int K, int N, int B, int width, uint32_t *code, int64_t code_cap,
+                                 int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
 {
+    if (!tsg::jit_width_ok(width) || (B && width != tsg::kJitNW)) {
+        g_tsg_host_err = "tsg_jit_codegen: unsupported stream width " + std::to_string(width) +
+                         (B ? " for BlockedTCSC (64 only)" : " (64, 32, 16 or 8)");
+        return TSG_ERR_ARG;
+    }
     const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, B);
     if (!e.empty()) {
         g_tsg_host_err = std::string(B ? "tsg_jit_codegen: malformed BlockedTCSC: " : "tsg_jit_codegen: malformed TCSC: ") + e;
@@ -525,7 +536,7 @@ extern "C" int tsg_jit_codegen_blocked(const int32_t *csp, const int32_t *csn, c
         return TSG_ERR_ARG;
     }
     tsg::JitImage img;
-    tsg::build_jit_code(csp, csn, rip, rin, K, N, B, img);
+    tsg::build_jit_code(csp, csn, rip, rin, K, N, B, img, width);
     if (code_len) *code_len = (int64_t)img.code.size();
     if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
     if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
@@ -535,6 +546,15 @@ extern "C" int tsg_jit_codegen_blocked(const int32_t *csp, const int32_t *csn, c
     if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);
     if (wcode) std::memcpy(wcode, img.wcode.data(), img.wcode.size() * 4);
     return TSG_OK;
+}
+
+extern "C" int tsg_jit_codegen_blocked(const int32_t *csp, const int32_t *csn, const int32_t *rip,
+                                       const int32_t *rin, int K, int N, int B, uint32_t *code,
+                                       int64_t code_cap, int64_t *code_len, uint32_t *wcode, int64_t wcode_cap,
+                                       int64_t *wcode_len)
+{
+    return tsg_jit_codegen_w(csp, csn, rip, rin, K, N, B, tsg::kJitNW, code, code_cap, code_len, wcode, wcode_cap,
+                             wcode_len);
 }
 
 extern "C" int tsg_jit_codegen(const int32_t *csp, const int32_t *csn, const int32_t *rip,

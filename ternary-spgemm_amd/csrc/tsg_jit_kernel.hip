@@ -54,7 +54,14 @@ namespace {
 constexpr int kJWaves = TSG_JIT_GEOM == 2 ? 16 : 8;
 constexpr int kJMSplit = TSG_JIT_GEOM == 3 ? 2 : 1;
 constexpr int kJStreams = kJWaves / kJMSplit;
-constexpr int kJNW = TSG_JIT_GEOM == 2 ? 32 : 64;
+// TSG_JIT_NW: a narrower stream width on geometry 1 (32, 16 or 8 columns per
+// wave; lib/tsg_jit_w<NW>.co) -- more workgroups for small M, same registers
+#ifndef TSG_JIT_NW
+#define TSG_JIT_NW (TSG_JIT_GEOM == 2 ? 32 : 64)
+#endif
+constexpr int kJNW = TSG_JIT_NW;
+static_assert(TSG_JIT_GEOM == 1 || kJNW == (TSG_JIT_GEOM == 2 ? 32 : 64), "narrow widths: geometry 1 only");
+static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8, "stream width");
 constexpr int kJTileM = TSG_JIT_GEOM == 3 ? 256 : 128;
 constexpr int kJTileCols = kJStreams * kJNW;
 constexpr int kJChunk = TSG_JIT_GEOM == 3 ? 48 : 96;
@@ -64,6 +71,7 @@ constexpr int kJPieces = kJChunk / kJPieceRows / kJWaves;  // LDS-DMA pieces per
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
+typedef float F32x16 __attribute__((ext_vector_type(16)));
 
 #if TSG_JIT_GEOM != 2
 #define TSG_JIT_CLOBBERS \
@@ -160,7 +168,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const uint32_t l128 = (uint32_t)lane * 128u;
     const uint32_t stride = (uint32_t)kJChunk * (uint32_t)Mp * 4u;
 
-#if TSG_JIT_GEOM != 2
+#if TSG_JIT_GEOM != 2 && TSG_JIT_NW == 64
     F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
     asm volatile("s_getpc_b64 s[94:95]\n"
                  ".Ljr%=:\n\t"
@@ -177,6 +185,48 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
         return c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
              : c < 48 ? a2[2 * (c & 15) + r] : a3[2 * (c & 15) + r];
     };
+#elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 32
+    F32x32 a0 = {}, a1 = {};  // comp.h:41
+    asm volatile("s_getpc_b64 s[94:95]\n"
+                 ".Ljr%=:\n\t"
+                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
+                 "s_addc_u32 s95, s95, 0\n\t"
+                 "s_setpc_b64 %[cp]\n"
+                 ".Ljb%=:"
+                 : "+{v[116:147]}"(a0), "+{v[148:179]}"(a1)
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
+                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
+                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                 : TSG_JIT_CLOBBERS);
+    auto acc_of = [&](int c, int r) { return c < 16 ? a0[2 * (c & 15) + r] : a1[2 * (c & 15) + r]; };
+#elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 16
+    F32x32 a0 = {};  // comp.h:41
+    asm volatile("s_getpc_b64 s[94:95]\n"
+                 ".Ljr%=:\n\t"
+                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
+                 "s_addc_u32 s95, s95, 0\n\t"
+                 "s_setpc_b64 %[cp]\n"
+                 ".Ljb%=:"
+                 : "+{v[116:147]}"(a0)
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
+                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
+                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                 : TSG_JIT_CLOBBERS);
+    auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
+#elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 8
+    F32x16 a0 = {};  // comp.h:41
+    asm volatile("s_getpc_b64 s[94:95]\n"
+                 ".Ljr%=:\n\t"
+                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
+                 "s_addc_u32 s95, s95, 0\n\t"
+                 "s_setpc_b64 %[cp]\n"
+                 ".Ljb%=:"
+                 : "+{v[116:131]}"(a0)
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
+                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
+                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                 : TSG_JIT_CLOBBERS);
+    auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
 #else
     F32x32 a0 = {}, a1 = {};  // comp.h:41
     asm volatile("s_getpc_b64 s[94:95]\n"

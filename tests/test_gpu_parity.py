@@ -84,6 +84,44 @@ def test_edges_vs_oracle(tsg, oracle_mod, M, K, N, s):
         assert _bits_eq(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
 
 
+@pytest.mark.parametrize("width", [64, 32, 16, 8])
+def test_every_stream_width_vs_oracle(tsg, oracle_mod, width):
+    """Each jit stream width (tcsc_hip_set_jit_width) pinned, on ragged shapes,
+    bit for bit against the oracle (integer and order-sensitive X, PReLU)."""
+    O = oracle_mod
+    for M, K, N, s in ((1, 64, 96, 2), (129, 257, 65, 4), (300, 1000, 129, 16), (200, 96, 700, 4)):
+        W = O.gen_ternary(K, N, s, M + K + width)
+        t = O.tcsc_encode(W)
+        h = tsg.TCSCDevice(*t.arrays, K, N)
+        h.set_jit_width(width)
+        assert h.jit_width(M) == width
+        b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
+        alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
+        for X in (O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)):
+            assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b)), (M, K, N, s, width)
+            assert _bits_eq(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
+        h.close()
+
+
+def test_auto_width_small_m(tsg, oracle_mod):
+    """Automatic width: narrow streams for small M, the default 64 at config
+    3's M; one handle switching widths call by call stays bit-exact."""
+    O = oracle_mod
+    K, N = 1024, 4096
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 77))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    assert h.jit_width(32) < 64 and h.jit_width(8192) == 64
+    b = np.full(N, 2.0, np.float32)
+    for M in (32, 8192, 7):
+        X = O.init_x_frac(M, K, M)
+        Y = h.gemm(X, b)
+        rows = slice(0, 64)
+        assert _bits_eq(Y[rows], O.base_tcsc(X[rows], t, b)), M
+    with pytest.raises(tsg.TSGError):
+        h.set_jit_width(24)
+    h.close()
+
+
 def test_structural_edges(tsg, oracle_mod):
     """All-zero W, fully dense ternary W, empty and full columns, K=0."""
     O = oracle_mod

@@ -244,10 +244,11 @@ def emulate(code, wcode, X, K, N):
     return Y[:M, :N]
 
 
-def _check(tsg, O, M, K, N, s, seed, frac, W=None):
+def _check(tsg, O, M, K, N, s, seed, frac, W=None, width=64):
     W = O.gen_ternary(K, N, s, seed) if W is None else W
     t = O.tcsc_encode(W)
-    code, wcode = tsg.jit_codegen(*t.arrays, K, N)
+    code, wcode = tsg.jit_codegen(*t.arrays, K, N, width=width)
+    assert Geom(code).nw == width
     X = O.init_x_frac(M, K, seed + 1) if frac else O.init_x_int(M, K, seed + 1)
     b = np.linspace(-2, 3, N).astype(np.float32)
     Y = emulate(code, wcode, X, K, N) + b
@@ -264,6 +265,25 @@ def _check(tsg, O, M, K, N, s, seed, frac, W=None):
 def test_jit_code_emulates_base_tcsc(tsg, oracle_mod, M, K, N, s):
     for frac in (False, True):
         _check(tsg, oracle_mod, M, K, N, s, 11 + K + N, frac)
+
+
+@pytest.mark.parametrize("width", [32, 16, 8])
+@pytest.mark.parametrize("M,K,N,s", [(5, 70, 33, 2), (130, 200, 150, 4), (3, 97, 9, 16)])
+def test_jit_code_narrow_streams(tsg, oracle_mod, M, K, N, s, width):
+    """Narrow streams (small-M widths, tsg_capi.cpp pick_jit_width): same
+    register contract, fewer accumulators, more column tiles; same order."""
+    for frac in (False, True):
+        _check(tsg, oracle_mod, M, K, N, s, 5 + K + N + width, frac, width=width)
+
+
+def test_jit_width_rejected(tsg, oracle_mod):
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(64, 20, 4, 1))
+    with pytest.raises(tsg.TSGError, match="width"):
+        tsg.jit_codegen(*t.arrays, 64, 20, width=24)
+    blk = O.blocked_tcsc_encode(O.gen_ternary(64, 20, 4, 1), 16)
+    with pytest.raises(tsg.TSGError, match="BlockedTCSC"):
+        tsg.jit_codegen(*blk, 64, 20, B=16, width=16)
 
 
 def test_jit_code_dense_and_empty_columns(tsg, oracle_mod):
