@@ -113,6 +113,10 @@ public:
         check(tcsc_hip_gemm_prelu(h_.get(), X, B, alpha, Y, M, N, K), "tcsc_hip_gemm_prelu");
     }
 
+    // Work buffer + the code image calls with up to max_M rows run, prepared
+    // now (a first call would otherwise compile its stream width: tcsc_hip_reserve).
+    void reserve(int max_M) const { check(tcsc_hip_reserve(h_.get(), max_M), "tcsc_hip_reserve"); }
+
     tsg_tcsc *handle() const { return h_.get(); }
     int K() const { return K_; }
     int N() const { return N_; }
