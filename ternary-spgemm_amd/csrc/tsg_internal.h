@@ -118,7 +118,7 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 // TCSC arrays (tsg_jit.cpp).  A workgroup covers kJitTileM M rows (2 per lane)
 // x kJitTileCols columns; each generated stream owns kJitNW columns and is run
 // by kJitMSplit waves (one per 128-row M slice); X^T chunks of kJitChunk K rows
-// in a ring of 3 LDS buffers (144 KiB).  Geometry (compile time, TSG_JIT_GEOM,
+// in a ring of kJitRing LDS buffers (3 x 48 KiB; ring 2: 2 x 64 KiB).  Geometry (compile time, TSG_JIT_GEOM,
 // shared with tsg_jit_kernel.hip):
 //   1 (default): 8 waves x 64 columns x 128 M rows, 48 X slots, 2 waves/SIMD
 //   2:          16 waves x 32 columns x 128 M rows, 24 X slots, 4 waves/SIMD
@@ -133,7 +133,16 @@ constexpr int kJitMSplit = TSG_JIT_GEOM == 3 ? 2 : 1;
 constexpr int kJitStreams = kJitWaves / kJitMSplit;     // streams per column tile
 constexpr int kJitNW = TSG_JIT_GEOM == 2 ? 32 : 64;
 constexpr int kJitTileCols = kJitStreams * kJitNW;
-constexpr int kJitChunk = TSG_JIT_GEOM == 3 ? 48 : 96;
+// TSG_JIT_RING: LDS buffers in the X^T ring.  3 (default): 96-row chunks, each
+// staged two steps ahead; 2 (geometry 1 only): 128-row chunks (2 x 64 KiB),
+// staged one step ahead -- a third fewer steps (barriers), no read-ahead
+// across a barrier.
+#ifndef TSG_JIT_RING
+#define TSG_JIT_RING 3
+#endif
+constexpr int kJitRing = TSG_JIT_RING;
+static_assert(kJitRing == 3 || (kJitRing == 2 && TSG_JIT_GEOM == 1), "2-buffer ring: geometry 1 only");
+constexpr int kJitChunk = TSG_JIT_GEOM == 3 ? 48 : kJitRing == 2 ? 128 : 96;
 constexpr int kJitSlots = TSG_JIT_GEOM == 2 ? 24 : 48;  // X slot registers v[8 : 8 + 2 * slots)
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
 

@@ -106,7 +106,7 @@ struct Emit {
     uint32_t pos_bytes() const { return (uint32_t)(c.size() * 4); }
 };
 
-// Register contract (tsg_jit_kernel.hip): X slots v[8 : 8 + 2S), then 3 LDS
+// Register contract (tsg_jit_kernel.hip): X slots v[8 : 8 + 2S), then kJitRing LDS
 // buffer bases, the code-prefetch sink, the DMA piece offsets, lane*128, and
 // the accumulators from the next even register.
 constexpr uint32_t kRowBytes = kJitTileM * 4;             // one X^T row of the tile in LDS
@@ -116,7 +116,7 @@ constexpr int kPieces = kJitChunk / kPieceRows / kJitWaves;  // DMA pieces per w
 static_assert(kPieces * kPieceRows * kJitWaves == kJitChunk, "chunk rows split in pieces over the waves");
 constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 2s : 9 + 2s]
 constexpr uint32_t kLdsBaseV = kXSlot0 + 2 * kJitSlots;   // + b: lane row 0 of LDS buffer b
-constexpr uint32_t kSinkV = kLdsBaseV + 3;
+constexpr uint32_t kSinkV = kLdsBaseV + kJitRing;
 constexpr uint32_t kDmaOffV = kSinkV + 1;                  // + i: DMA piece i offsets
 constexpr uint32_t kLane128V = kDmaOffV + kPieces;
 constexpr uint32_t kAcc0 = (kLane128V + 2) & ~1u;         // column c: v[acc0 + 2c : acc0 + 2c + 1]
@@ -132,7 +132,7 @@ struct Section {
     std::vector<std::vector<uint8_t>> cols;
 };
 
-// One step of a stream: the X^T chunk staged into LDS buffer q % 3 and which
+// One step of a stream: the X^T chunk staged into LDS buffer q % kJitRing and which
 // of its entries the step adds.
 struct StepSpec {
     int chunk;       // X^T chunk (kJitChunk rows)
@@ -203,7 +203,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     code.insert(code.end(), {kJitMagic0, kJitMagic1,
                              (uint32_t)kJitWaves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
-                             (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S, 0u});
+                             (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
+                             (uint32_t)kJitRing});
     Emit E{code};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
@@ -248,7 +249,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             }
     };
     int base_chunk = -1;  // chunk whose base s[84:85] holds
-    // stage step q's chunk into LDS buffer q % 3; M0 = s83 (this wave's first
+    // stage step q's chunk into LDS buffer q % kJitRing; M0 = s83 (this wave's first
     // piece, set by the dispatcher) + buffer + piece offset
     auto emit_dma = [&](int q) {
         if (d_nodma) return;
@@ -262,7 +263,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         base_chunk = j;
         E.nop(4);  // SALU-written SGPR base -> VMEM
         for (int i = 0; i < kPieces; i++) {
-            E.m0_wave((uint32_t)(q % 3) * kBufBytes + (uint32_t)i * 1024u);
+            E.m0_wave((uint32_t)(q % kJitRing) * kBufBytes + (uint32_t)i * 1024u);
             E.nop(0);  // M0 -> LDS-DMA
             E.glds_x4(kDmaOffV + (uint32_t)i);
         }
@@ -278,6 +279,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // Every column meets its rows in ascending k either way.
     // TSG_JIT_READS="G,RA,order" (order 0 = column-major, 1 = row-major);
     // default S/2,S/2,0 (the block schedule: one group of reads in flight).
+    // Reads run ahead into the next step only when its chunk is already
+    // resident (ring 3: staged two steps ahead, visible since the last barrier);
+    // with 2 buffers the next chunk lands at this step's closing barrier.
+    const int kLook = kJitRing == 3 ? 1 : 0;
     int G = S / 2, RA = S / 2, row_major = 0;
     if (const char *rv = std::getenv("TSG_JIT_READS")) std::sscanf(rv, "%d,%d,%d", &G, &RA, &row_major);
     if (G < 1 || RA < 0 || G + RA > S) {
@@ -292,10 +297,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
             E.save_m0();
-            // prologue: steps 0 and 1 staged, landed, visible
+            // prologue: the first kJitRing - 1 steps staged, landed, visible
             if (steps > 0) {
-                emit_dma(0);
-                if (steps > 1) emit_dma(1);
+                for (int q = 0; q < std::min(steps, kJitRing - 1); q++) emit_dma(q);
                 E.wait_vm0();
                 E.barrier();
             }
@@ -319,7 +323,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     if (issued >= first[rq + 1]) return;  // past step qmax
                     const int r = secs[rq].rows[(size_t)(issued - first[rq])];
                     if (!d_noreads && !(d_halfreads && (issued & 1)))
-                        E.ds_read_b64(kXSlot0 + 2u * (uint32_t)(issued % S), kLdsBaseV + (uint32_t)(rq % 3),
+                        E.ds_read_b64(kXSlot0 + 2u * (uint32_t)(issued % S), kLdsBaseV + (uint32_t)(rq % kJitRing),
                                       (uint32_t)r * kRowBytes);
                 }
             };
@@ -348,7 +352,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         live[col] = 1;
                     }
                 };
-                if (q + 2 < steps) emit_dma(q + 2);
+                if (q + kJitRing - 1 < steps) emit_dma(q + kJitRing - 1);
                 // code touches go out AFTER the step's DMA: VMEM loads return in
                 // order, so the step's closing vmcnt(ntouch) waits for every DMA
                 // piece but lets the touches (L2 misses) run into the next step
@@ -364,7 +368,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     const int64_t g1 = first[q] + i1;
                     issue_reads(g1, q);  // (only if the schedule left the group unread)
                     wait_rows(g1);
-                    issue_reads(g1 + RA, q + 1);
+                    issue_reads(g1 + RA, q + kLook);
                     if (row_major) {
                         for (int i = i0; i < i1; i++) {
                             const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % S);
@@ -390,7 +394,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                             E.pk_acc(kAcc0 + 2u * (uint32_t)col, kTmp0 + 2u * (uint32_t)(col - sp.c0));
                             live[col] = 0;
                         }
-                issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first rows
+                issue_reads(first[q + 1] + std::max(G, RA), q + kLook);  // next step's first rows (ring 3)
                 E.wait_vm(ntouch);
                 if (!d_nobar) E.barrier();
             }

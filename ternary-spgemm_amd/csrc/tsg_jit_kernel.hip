@@ -28,15 +28,18 @@
 // steps ahead, one `s_waitcnt vmcnt(0); s_barrier` per step (step q = pass
 // p * nch + chunk j: p = 0 the +1 entries, p = 1 the -1 entries), the next
 // step's first X rows read before the barrier, the stream's own code touched
-// ahead (L2 prefetch).  Register contract (tsg_jit.cpp), S X slots, P DMA pieces:
+// ahead (L2 prefetch).  TSG_JIT_RING=2: 128-row chunks in 2 buffers, staged one
+// step ahead, no read across a barrier.
+// Register contract (tsg_jit.cpp), S X slots, R ring buffers, P DMA pieces:
 //   v[8 : 8+2S)   X slots (2 M rows each)
-//   next 3        LDS byte address of lane row 0 in buffer 0/1/2
+//   next R        LDS byte address of lane row 0 in buffer 0..R-1
 //   next 1        code-prefetch sink
 //   next P        per-lane byte offsets (from the chunk base) of this wave's
 //                 LDS-DMA pieces (2 rows each)
 //   next 1        lane * 128 (code prefetch)
 //   from the next even register: accumulators, column c at acc0 + 2c
 //   GEOM 1: S=48 -> v104-106, v107, v108-113, v114, acc v[116:243]
+//   GEOM 1, ring 2: v104-105, v106, v107-114, v115, acc v[116:243]
 //   GEOM 2: S=24 -> v56-58,   v59,  v60-62,   v63,  acc v[64:127]
 //   s[80:81] X^T base, s82 chunk stride in bytes, s83 LDS byte offset of this
 //   wave's first DMA piece, s[84:85] chunk base (stream),
@@ -64,14 +67,34 @@ static_assert(TSG_JIT_GEOM == 1 || kJNW == (TSG_JIT_GEOM == 2 ? 32 : 64), "narro
 static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8, "stream width");
 constexpr int kJTileM = TSG_JIT_GEOM == 3 ? 256 : 128;
 constexpr int kJTileCols = kJStreams * kJNW;
-constexpr int kJChunk = TSG_JIT_GEOM == 3 ? 48 : 96;
-constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB
+#ifndef TSG_JIT_RING
+#define TSG_JIT_RING 3
+#endif
+constexpr int kJRing = TSG_JIT_RING;  // LDS buffers in the X^T ring (tsg_internal.h)
+static_assert(kJRing == 3 || (kJRing == 2 && TSG_JIT_GEOM == 1), "2-buffer ring: geometry 1 only");
+constexpr int kJChunk = TSG_JIT_GEOM == 3 ? 48 : kJRing == 2 ? 128 : 96;
+constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB (ring 2: 64 KiB)
 constexpr int kJPieceRows = 1024 / (kJTileM * 4);    // X^T rows per 1-KiB LDS-DMA piece
 constexpr int kJPieces = kJChunk / kJPieceRows / kJWaves;  // LDS-DMA pieces per wave per chunk
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 typedef float F32x16 __attribute__((ext_vector_type(16)));
+
+// geometry 1/3 register bindings of the LDS bases, DMA piece offsets, lane*128
+// and the code-prefetch sink (tsg_jit.cpp kLdsBaseV...kLane128V)
+#if TSG_JIT_RING == 2
+#define TSG_JIT_IN                                                                                  \
+    "{v104}"(lb0), "{v105}"(lb1), "{v107}"(off[0]), "{v108}"(off[1]), "{v109}"(off[2]),          \
+        "{v110}"(off[3]), "{v111}"(off[4]), "{v112}"(off[5]), "{v113}"(off[6]), "{v114}"(off[7]), \
+        "{v115}"(l128)
+#define TSG_JIT_SINK "v106"
+#else
+#define TSG_JIT_IN                                                                                  \
+    "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),             \
+        "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+#define TSG_JIT_SINK "v107"
+#endif
 
 #if TSG_JIT_GEOM != 2
 #define TSG_JIT_CLOBBERS \
@@ -82,7 +105,7 @@ typedef float F32x16 __attribute__((ext_vector_type(16)));
         "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", \
         "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", \
         "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", \
-        "v100", "v101", "v102", "v103", "v107", "s84", "s85", "s86", "s88", "s89", "s94", "s95", \
+        "v100", "v101", "v102", "v103", TSG_JIT_SINK, "s84", "s85", "s86", "s88", "s89", "s94", "s95", \
         "scc", "memory"
 #else
 #define TSG_JIT_CLOBBERS \
@@ -100,7 +123,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) char lds[3 * kJBufBytes];
+    __shared__ __attribute__((aligned(16))) char lds[kJRing * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
     // LDS is only addressed from the generated code, at absolute offsets from
     // 0 (the only LDS object): this use keeps the allocation in the descriptor
@@ -155,7 +178,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
 #else
     const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJStreams + stream]);
 #endif
-    const uint32_t lb0 = (uint32_t)(ms * 512 + lane * 8), lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
+    const uint32_t lb0 = (uint32_t)(ms * 512 + lane * 8), lb1 = lb0 + kJBufBytes;
+    [[maybe_unused]] const uint32_t lb2 = lb0 + 2 * kJBufBytes;  // ring 3 only
     // LDS-DMA piece i of this wave: chunk rows kJPieceRows*(wave*P + i) + lane / (64 / kJPieceRows)
     constexpr int kLanesPerRow = 64 / kJPieceRows;
     uint32_t off[kJPieces];
@@ -178,8 +202,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  ".Ljb%=:"
                  : "+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3)
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
-                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                   TSG_JIT_IN
                  : TSG_JIT_CLOBBERS);
     auto acc_of = [&](int c, int r) {
         return c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
@@ -195,8 +218,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  ".Ljb%=:"
                  : "+{v[116:147]}"(a0), "+{v[148:179]}"(a1)
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
-                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                   TSG_JIT_IN
                  : TSG_JIT_CLOBBERS);
     auto acc_of = [&](int c, int r) { return c < 16 ? a0[2 * (c & 15) + r] : a1[2 * (c & 15) + r]; };
 #elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 16
@@ -209,8 +231,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  ".Ljb%=:"
                  : "+{v[116:147]}"(a0)
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
-                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                   TSG_JIT_IN
                  : TSG_JIT_CLOBBERS);
     auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
 #elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 8
@@ -223,8 +244,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  ".Ljb%=:"
                  : "+{v[116:131]}"(a0)
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),
-                   "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+                   TSG_JIT_IN
                  : TSG_JIT_CLOBBERS);
     auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
 #else

@@ -14,7 +14,6 @@ shows the GPU runs that code."""
 import numpy as np
 import pytest
 
-NBUF = 3
 MAGIC = (0x7453474A, 0x314A4954)
 
 
@@ -33,8 +32,9 @@ class Geom:
         self.buf_bytes = self.chunk * self.row_bytes
         self.piece_rows = 1024 // self.row_bytes
         self.pieces = self.chunk // self.piece_rows // self.waves
+        self.ring = int(code[7]) or 3  # LDS buffers in the X^T ring (TSG_JIT_RING)
         self.lds_v = 8 + 2 * self.slots
-        self.sink_v = self.lds_v + 3
+        self.sink_v = self.lds_v + self.ring
         self.dma_v = self.sink_v + 1
         self.l128_v = self.dma_v + self.pieces
         self.acc0 = (self.l128_v + 2) & ~1
@@ -129,6 +129,7 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
     region_bytes = len(code) * 4
     stride = CHUNK * Mp * 4
     lanes = np.arange(64)
+    NBUF = G.ring
     lds = np.zeros(NBUF * BUF_BYTES // 4, np.float32)
     landed = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)   # phase a row's data landed
     last_read = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)
@@ -195,7 +196,7 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                     vd, a, off = f
                     assert vd not in wv.reads, "X slot reloaded before its previous read was waited for"
                     wv.reads.append(vd)
-                    assert G.lds_v <= a < G.lds_v + 3 and off % ROW_BYTES == 0 and off // ROW_BYTES < CHUNK
+                    assert G.lds_v <= a < G.lds_v + NBUF and off % ROW_BYTES == 0 and off // ROW_BYTES < CHUNK
                     assert 8 <= vd < 8 + 2 * G.xslots
                     row = (a - G.lds_v) * CHUNK + off // ROW_BYTES
                     assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
