@@ -64,10 +64,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and rank == 0:
         print(f"# note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # one process per GPU; the modulo only matters for a multi-rank rehearsal
+    # on a box with fewer GPUs (TSG_BENCH_BACKEND=gloo: RCCL refuses two ranks
+    # on one device)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("TSG_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     M, K, Nr, s = a.M, a.K, a.N, a.s
     Ntot = Nr * world
