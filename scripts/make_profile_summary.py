@@ -57,7 +57,7 @@ for kn, v in tot.items():
         o["lds_util"] = per["SQ_LDS_IDX_ACTIVE"] / (per["GRBM_GUI_ACTIVE"] / 8 * 256)
     out["kernels"][kn] = o
     main = kn.split("::")[-1].split("<")[0]
-    if main != "tsg_transpose_kernel" and "hbm_bytes" in o:  # the TCSC kernel
+    if "transpose" not in main and "hbm_bytes" in o:  # the TCSC kernel
         out["kernel"] = main
         out["per_launch_hbm_bytes"][out["workload"]] = o["hbm_bytes"]
 json.dump(out, open(dst + "_pmc_summary.json", "w"), indent=1)
