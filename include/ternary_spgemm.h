@@ -98,8 +98,15 @@ int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, 
 
 /* DEVICE pointers (on the handle's device), enqueued on `stream`
  * (a hipStream_t; NULL = legacy default stream); returns without waiting.
- * The work buffer must be reserved for this M beforehand (tcsc_hip_reserve)
- * for the call to be graph-capturable; otherwise it is grown on demand. */
+ * Streams: calls on one handle are serialised on the host (a mutex) and share
+ * the handle's X^T work buffer; a call on a different stream than the
+ * previous call waits (hipStreamWaitEvent) for the previous call's kernel
+ * before it overwrites that buffer, so calls from several streams / threads
+ * on one handle are safe (and run one after the other on the device).
+ * Graph capture: after tcsc_hip_reserve(h, max_M), calls with M <= max_M
+ * allocate, compile and synchronise nothing and can be captured; a captured
+ * call reuses the work buffer when replayed, so a replay must not overlap
+ * other calls on the same handle issued on other streams. */
 int tcsc_hip_gemm_dev(tsg_tcsc *h, const float *dX, const float *db, float *dY,
                       int M, int N, int K, void *stream);
 
@@ -111,8 +118,9 @@ int tcsc_hip_gemm_prelu_dev(tsg_tcsc *h, const float *dX, const float *db, const
                             float *dY, int M, int N, int K, void *stream);
 
 /* Pre-allocates the per-handle work buffer for row counts up to max_M and, on
- * the weight-compiled kernel, compiles the code image a call with max_M rows
- * runs (tcsc_hip_jit_width), so no later call compiles (graph capture). */
+ * the weight-compiled kernel, compiles every code image a call with M <= max_M
+ * rows runs (tcsc_hip_jit_width), so no later such call allocates or compiles
+ * (graph capture). */
 int tcsc_hip_reserve(tsg_tcsc *h, int max_M);
 
 /* Weight-compiled kernel: columns per generated stream (a wave's columns).
@@ -149,8 +157,10 @@ int tcsc_hip_set_timing(tsg_tcsc *h, int enable);
 int tcsc_hip_kernel_time(tsg_tcsc *h, double *total_ms, int64_t *launches, int reset);
 
 /* Name of the device kernel this handle launches (the one timed above):
- * "tsg_jit_kernel" (default: W compiled into gfx950 code at registration) or,
- * when TSG_KERNEL selects another family at registration, that kernel. */
+ * "tsg_jit_kernel" (default: W compiled into gfx950 code at registration) or
+ * "tsg_tcsc_rx_kernel" (the register-X walk: W too large for one compiled
+ * image, a generated image the loader refused -- logged on stderr -- or
+ * TSG_KERNEL=rx at registration). */
 const char *tcsc_hip_kernel_name(const tsg_tcsc *h);
 
 const char *tcsc_hip_last_error(void);

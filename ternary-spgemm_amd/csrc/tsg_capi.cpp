@@ -33,12 +33,10 @@ struct tsg_tcsc {
     int K = 0, N = 0, device = 0;
     int B = 0;                            // BlockedTCSC<B> block size (0: plain TCSC)
     int64_t nnz_pos = 0, nnz_neg = 0;
-    // kernel family: TSG_KERNEL=chunked (round-1 v1), pair / flat (LDS-gather
-    // stream kernel, two walks), rx (register-X kernel), jit (weight-compiled)
-    enum Kind { kChunked, kStream, kRx, kJit } kind = kStream;
-    bool stream_kernel = true;            // kind == kStream
-    tsg::Image img;                       // v1 device image (chunked kernel)
-    tsg::StreamImage simg;                // device image of the stream kernel
+    // kernel family: jit (weight-compiled, default) or rx (register-X walk:
+    // images too large for 32-bit stream offsets, a failed image load, or
+    // TSG_KERNEL=rx)
+    enum Kind { kRx, kJit } kind = kJit;
     tsg::RxImage rimg;                    // device image of the rx kernel
     // jit kernel: one compiled image per stream width (index tsg::kJitWidths):
     // the default width at registration, narrower ones on the first call with
@@ -47,7 +45,6 @@ struct tsg_tcsc {
         int nw = 0, Npad = 0;
         tsg::JitModule mod;               // dispatcher + generated code, loaded
         uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
-        bool checked = false;             // status read back once after the first launch
         int64_t code_bytes = 0, wcode_words = 0;
     };
     JitVariant jv[4];
@@ -57,8 +54,13 @@ struct tsg_tcsc {
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
-    float *d_zero = nullptr;              // 256 B of +0.0f (source of the LDS zero rows)
     size_t work_bytes = 0;
+    // d_work is shared by every call on the handle: the last stream that read
+    // it and an event recorded after that read; a call on another stream
+    // waits for the event before it overwrites X^T (run_dev)
+    hipStream_t work_stream = nullptr;
+    hipEvent_t work_ev = nullptr;
+    bool work_used = false;
     // host-pointer path staging (tcsc_hip_gemm): grow-only
     float *d_x = nullptr, *d_b = nullptr, *d_y = nullptr, *d_alpha = nullptr;
     size_t x_bytes = 0, y_bytes = 0;
@@ -101,24 +103,32 @@ int check_device(int dev)
 
 int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp)
 {
-    const int tm = h->kind == tsg_tcsc::kRx ? tsg::kRxTileM : h->kind == tsg_tcsc::kJit ? tsg::kJitTileM : tsg::kTileM;
+    const bool jit = h->kind == tsg_tcsc::kJit;
+    const int tm = jit ? tsg::kJitTileM : tsg::kRxTileM;
     Mp = ((std::max(M, 1) + tm - 1) / tm) * tm;
-    Kp = h->kind == tsg_tcsc::kJit      ? h->jit_nch * tsg::kJitChunk
-         : h->kind == tsg_tcsc::kRx     ? h->rimg.nch * tsg::kRxChunk
-         : h->kind == tsg_tcsc::kStream ? h->simg.nch * tsg::kSChunk
-                                        : h->img.nch * tsg::kChunkK;
+    Kp = jit ? h->jit_nch * tsg::kJitChunk : h->rimg.nch * tsg::kRxChunk;
     return TSG_OK;
 }
 
-int ensure_work(tsg_tcsc *h, int M)
+// Grows the X^T work buffer (grow-only).  A grow frees the old buffer, so it
+// first waits for every launch that may still read it; it cannot happen while
+// a stream is being captured (tcsc_hip_reserve(max_M) before the capture).
+int ensure_work(tsg_tcsc *h, int M, bool capturing)
 {
     int Mp, Kp;
     dims_for(h, M, Mp, Kp);
     const size_t need = (size_t)Mp * Kp * sizeof(float);
     if (need <= h->work_bytes) return TSG_OK;
-    if (h->d_work) HIP_TRY(hipFree(h->d_work));
+    if (capturing)
+        return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " needs a larger work buffer during stream capture; "
+                                 "call tcsc_hip_reserve(h, max_M) before capturing");
+    if (h->d_work) {
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipFree(h->d_work));
+    }
     h->d_work = nullptr;
     h->work_bytes = 0;
+    h->work_used = false;
     if (hipMalloc(&h->d_work, need) != hipSuccess)
         return fail(TSG_ERR_NOMEM, "hipMalloc of " + std::to_string(need) + " B work buffer failed");
     h->work_bytes = need;
@@ -207,6 +217,10 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
     tsg::JitImage img;
     tsg::build_jit_code(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
                         h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw);
+    // stream offsets (wcode) and the dispatcher's region literal are 32-bit
+    if ((uint64_t)img.code.size() * 4 >= (1ull << 32) - (1ull << 20))
+        return fail(TSG_ERR_RANGE, "jit image of " + std::to_string((uint64_t)img.code.size() * 4) +
+                                       " B exceeds the 32-bit stream offsets; shard W's columns");
     if (nw == tsg::kJitNW)
         if (const char *d = std::getenv("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
             const size_t S = tsg::kJitStreams;
@@ -231,6 +245,30 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
         v.mod.unload();
         return fail(TSG_ERR_HIP, "upload of the jit stream table failed");
     }
+    // probe launch: the dispatcher checks that its patched literal reaches the
+    // generated region (magic header) and reports it; nothing else runs.  Done
+    // here, at registration / reserve, so calls never read the status back
+    // (they stay asynchronous and graph-capturable).
+    if (!h->d_status && hipMalloc(&h->d_status, 16) != hipSuccess) {
+        (void)hipFree(v.d_wcode);
+        v.d_wcode = nullptr;
+        v.mod.unload();
+        return fail(TSG_ERR_NOMEM, "hipMalloc of the jit status word failed");
+    }
+    uint32_t st[2] = {0xffffffffu, 0u};
+    const int tile_cols = nw * tsg::kJitStreams;
+    bool ok = hipMemset(h->d_status, 0, 16) == hipSuccess &&
+              tsg::launch_tcsc_jit(v.mod, nullptr, tsg::kJitTileM, v.d_wcode, nullptr, nullptr, nullptr, 0, 0,
+                                   tile_cols, img.nch, 2, h->d_status, tile_cols, nullptr) == 0 &&
+              hipStreamSynchronize(nullptr) == hipSuccess &&
+              hipMemcpy(st, h->d_status, sizeof st, hipMemcpyDeviceToHost) == hipSuccess;
+    if (!ok || st[0] != 0 || st[1] != tsg::kJitMagic0) {
+        (void)hipFree(v.d_wcode);
+        v.d_wcode = nullptr;
+        v.mod.unload();
+        return fail(TSG_ERR_HIP, "jit kernel (width " + std::to_string(nw) + "): probe launch did not find the "
+                                 "generated code region (status " + std::to_string(st[0]) + ")");
+    }
     v.nw = nw;
     v.Npad = img.Npad;
     v.code_bytes = (int64_t)img.code.size() * 4;
@@ -252,91 +290,67 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     if (!dY || !db || (K > 0 && !dX) || (prelu && !dalpha))
         return fail(TSG_ERR_ARG, "null device pointer");
     DeviceGuard g(h->device);
-    int rc = ensure_work(h, M);
+    // One call at a time per handle: the X^T work buffer, the jit images and
+    // the timing ring are shared by every stream that uses the handle.
+    std::lock_guard<std::mutex> lk(h->mu);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(s, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    int rc = ensure_work(h, M, capturing);
     if (rc) return rc;
     int Mp, Kp;
     dims_for(h, M, Mp, Kp);
     tsg_tcsc::JitVariant *jv = nullptr;
     if (h->kind == tsg_tcsc::kJit) {
         const int nw = pick_jit_width(h, M);
-        {
-            std::lock_guard<std::mutex> lk(h->mu);
-            rc = ensure_jit_variant(h, nw);
-        }
-        if (rc) return rc;
         jv = &h->jv[width_index(nw)];
+        if (!jv->mod.function && capturing)
+            return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(nw) +
+                                         " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
+        rc = ensure_jit_variant(h, nw);
+        if (rc) return rc;
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
         const int64_t wgs = (int64_t)(Mp / tsg::kJitTileM) * (jv->Npad / (jv->nw * tsg::kJitStreams));
         if ((int64_t)Mp * tsg::kJitChunk * 4 >= (1ll << 31) || wgs * tsg::kJitWaves * 64 >= (1ll << 32))
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " is too large for one jit launch; split the rows");
     }
+    // X^T of the previous call may still be read by its kernel on another
+    // stream: this call's staging waits for it (same stream: stream order)
+    if (!capturing && h->work_used && h->work_stream != s) HIP_TRY(hipStreamWaitEvent(s, h->work_ev, 0));
     if (K == 0) {
         // no X at all: chain is +0; X^T stays zero
         HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
     } else if (tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s) != 0) {
         return fail(TSG_ERR_HIP, std::string("transpose launch: ") + hipGetErrorString(hipGetLastError()));
     }
-    std::lock_guard<std::mutex> lk(h->mu);
     int slot = -1;
-    if (h->timing) {
+    if (h->timing && !capturing) {
         rc = harvest_timing(h, false);
         if (rc) return rc;
         slot = h->ring_head;
         HIP_TRY(hipEventRecord(h->ev0[slot], s));
     }
-    unsigned long long *stamps = nullptr;
-    size_t nstamp = 0;
-    if (h->kind != tsg_tcsc::kChunked && h->kind != tsg_tcsc::kJit && std::getenv("TSG_STAMPS")) {  // diagnostic path (never timed)
-        nstamp = h->kind == tsg_tcsc::kRx
-            ? (size_t)(Mp / tsg::kRxTileM) * (h->rimg.Npad / tsg::kRxTileCols) * tsg::kRxWaves * 4
-            : (size_t)(Mp / tsg::kTileM) * (h->simg.Npad / h->simg.tile_cols) * tsg::kSWaves * 4;
-        HIP_TRY(hipMalloc(&stamps, nstamp * 8));
-    }
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * tsg::kJitStreams, s)
-        : h->kind == tsg_tcsc::kRx
-        ? tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
-                              h->rimg.nch, prelu ? 1 : 0, stamps, s)
-        : h->stream_kernel
-        ? tsg::launch_tcsc_stream(h->d_work, Mp, h->d_seg, h->d_ent, h->d_zero, db, dalpha, dY, M, N,
-                                  h->simg.Npad, h->simg.nch, h->simg.nw, prelu ? 1 : 0, stamps,
-                                  h->simg.flat, s)
-        : tsg::launch_tcsc(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->img.Npad,
-                           h->img.nch, h->img.tile_cols, prelu ? 1 : 0, s);
+        : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
+                              h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)
         return fail(TSG_ERR_HIP, std::string("tcsc launch: ") + hipGetErrorString(hipGetLastError()));
-    if (stamps) {
-        std::vector<unsigned long long> hs(nstamp);
-        HIP_TRY(hipStreamSynchronize(s));
-        HIP_TRY(hipMemcpy(hs.data(), stamps, nstamp * 8, hipMemcpyDeviceToHost));
-        HIP_TRY(hipFree(stamps));
-        double work = 0, wait = 0, tot = 0, wmax = 0;
-        const size_t nw = nstamp / 4;
-        for (size_t i = 0; i < nw; i++) {
-            work += (double)hs[4 * i];
-            wait += (double)hs[4 * i + 1];
-            tot += (double)hs[4 * i + 2];
-            wmax = std::max(wmax, (double)hs[4 * i]);
-        }
-        std::fprintf(stderr, "[tsg stamps] waves=%zu mean cycles/wave: total %.0f walk %.0f (%.1f%%) "
-                             "barrier-wait %.0f (%.1f%%) max-walk %.0f steps=%d\n",
-                     nw, tot / nw, work / nw, 100 * work / tot, wait / nw, 100 * wait / tot, wmax,
-                     2 * (h->kind == tsg_tcsc::kRx ? h->rimg.nch : h->simg.nch));
-    }
-    if (jv && !jv->checked) {
-        // one-time check that the dispatcher found the generated region
-        uint32_t st = 0;
-        HIP_TRY(hipMemcpyAsync(&st, h->d_status, sizeof st, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (st != 0) return fail(TSG_ERR_HIP, "jit kernel: generated code region not found (status " + std::to_string(st) + ")");
-        jv->checked = true;
-    }
     if (slot >= 0) {
         HIP_TRY(hipEventRecord(h->ev1[slot], s));
         h->ring_head = (h->ring_head + 1) % tsg_tcsc::kRing;
         h->ring_count++;
+    }
+    if (capturing) {
+        // a captured call's reads happen at replay time: not tracked (a replay
+        // must not overlap calls on other streams, include/ternary_spgemm.h)
+        h->work_used = false;
+    } else {
+        HIP_TRY(hipEventRecord(h->work_ev, s));
+        h->work_stream = s;
+        h->work_used = true;
     }
     return TSG_OK;
 }
@@ -382,7 +396,8 @@ void free_handle(tsg_tcsc *h)
     if (!h) return;
     DeviceGuard g(h->device);
     if (h->ring_count) (void)hipDeviceSynchronize();
-    for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_zero, (void *)h->d_x,
+    if (h->work_ev) (void)hipEventDestroy(h->work_ev);
+    for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_x,
                     (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha, (void *)h->d_status})
         if (p) (void)hipFree(p);
     for (auto &v : h->jv) {
@@ -464,7 +479,11 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
         8.0 * 1.25 * ((double)h->nnz_pos + (double)h->nnz_neg) + 256.0 * (double)steps * (double)streams;
     const bool jit_fits = jit_est < 3.0 * (double)(1ull << 30);
     const std::string kname = kenv ? kenv : (jit_fits ? "jit" : "rx");
-    if (B && kname != "jit" && kenv) {
+    if (kname != "jit" && kname != "rx") {
+        delete h;
+        return fail(TSG_ERR_ARG, "TSG_KERNEL=" + kname + ": expected jit or rx");
+    }
+    if (B && kname != "jit") {
         delete h;
         return fail(TSG_ERR_ARG, "BlockedTCSC runs on the jit kernel only (TSG_KERNEL=" + kname + ")");
     }
@@ -473,17 +492,7 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
         return fail(TSG_ERR_ARG, "TSG_KERNEL=jit: W has too many nonzeros for one weight-compiled image "
                                  "(> ~300M); shard columns across handles or use TSG_KERNEL=rx");
     }
-    if (kname == "jit") h->kind = tsg_tcsc::kJit;
-    else if (kname == "rx") h->kind = tsg_tcsc::kRx;
-    else if (kname == "chunked") h->kind = tsg_tcsc::kChunked;
-    else if (kname == "stream" || kname == "pair" || kname == "flat") h->kind = tsg_tcsc::kStream;
-    else {
-        delete h;
-        return fail(TSG_ERR_ARG, "TSG_KERNEL=" + kname + ": expected jit, rx, stream, pair, flat or chunked");
-    }
-    h->stream_kernel = h->kind == tsg_tcsc::kStream;
-    const std::vector<uint32_t> *segv, *entv;
-    static const std::vector<uint32_t> kNoEntries(1, 0u);
+    h->kind = kname == "jit" ? tsg_tcsc::kJit : tsg_tcsc::kRx;
     if (h->kind == tsg_tcsc::kJit) {
         // TSG_JIT_NW=<64|32|16|8> pins the stream width (A/B); default: per call
         if (const char *wv = std::getenv("TSG_JIT_NW")) {
@@ -496,35 +505,37 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
         }
         const int rc0 = ensure_jit_variant(h, h->jit_force ? h->jit_force : tsg::kJitNW);
         if (rc0) {
-            free_handle(h);
-            return rc0;
+            // A generated image that the loader refuses (or whose probe launch
+            // does not find its region) falls back to the rx kernel, unless jit
+            // was asked for explicitly or the format needs it (BlockedTCSC).
+            if (rc0 != TSG_ERR_HIP || kenv || B) {
+                free_handle(h);
+                return rc0;
+            }
+            std::fprintf(stderr, "[ternary_spgemm] warning: weight-compiled image unavailable (%s); "
+                                 "falling back to the rx kernel\n", g_tsg_host_err.c_str());
+            h->kind = tsg_tcsc::kRx;
         }
-        segv = &kNoEntries;
-        entv = &kNoEntries;
-    } else if (h->kind == tsg_tcsc::kRx) {
-        tsg::build_rx_image(csp, csn, rip, rin, K, N, h->rimg);
-        segv = &h->rimg.wstart;
-        entv = &h->rimg.ent;
-    } else if (h->stream_kernel) {
-        tsg::plan_stream_image(csp, csn, rip, rin, K, N, kname == "flat", h->simg);
-        segv = &h->simg.wstart;
-        entv = &h->simg.ent;
-    } else {
-        tsg::build_image(csp, csn, rip, rin, K, N, tsg::pick_tile_cols(N), h->img);
-        segv = &h->img.seg;
-        entv = &h->img.ent;
     }
+    if (h->kind == tsg_tcsc::kRx) tsg::build_rx_image(csp, csn, rip, rin, K, N, h->rimg);
+    static const std::vector<uint32_t> kNoEntries(1, 0u);
+    const std::vector<uint32_t> *segv = h->kind == tsg_tcsc::kRx ? &h->rimg.wstart : &kNoEntries;
+    const std::vector<uint32_t> *entv = h->kind == tsg_tcsc::kRx ? &h->rimg.ent : &kNoEntries;
 
     DeviceGuard g(device);
     const size_t sb = segv->size() * sizeof(uint32_t), eb = entv->size() * sizeof(uint32_t);
     if (hipMalloc(&h->d_seg, sb) != hipSuccess || hipMalloc(&h->d_ent, eb) != hipSuccess ||
         hipMalloc(&h->d_b, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
         hipMalloc(&h->d_alpha, std::max<size_t>((size_t)N * sizeof(float), 4)) != hipSuccess ||
-        hipMalloc(&h->d_zero, 256) != hipSuccess || hipMalloc(&h->d_status, 16) != hipSuccess) {
+        (!h->d_status && hipMalloc(&h->d_status, 16) != hipSuccess)) {
         free_handle(h);
         return fail(TSG_ERR_NOMEM, "hipMalloc of the device image failed");
     }
-    if (hipMemset(h->d_zero, 0, 256) != hipSuccess || hipMemset(h->d_status, 0, 16) != hipSuccess ||
+    if (hipEventCreateWithFlags(&h->work_ev, hipEventDisableTiming) != hipSuccess) {
+        free_handle(h);
+        return fail(TSG_ERR_HIP, "hipEventCreate of the work-buffer event failed");
+    }
+    if (hipMemset(h->d_status, 0, 16) != hipSuccess ||
         hipMemcpy(h->d_seg, segv->data(), sb, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(h->d_ent, entv->data(), eb, hipMemcpyHostToDevice) != hipSuccess) {
         free_handle(h);
@@ -625,14 +636,23 @@ extern "C" int tcsc_hip_create_csc_packed(const int32_t *col_ptr, const int32_t 
 
 extern "C" void tcsc_hip_destroy(tsg_tcsc *h) { free_handle(h); }
 
+// Prepares every call with M <= max_M: the work buffer for max_M rows and the
+// image of every stream width such a call picks (pick_jit_width depends on M
+// only through the number of 128-row M tiles).  After it, calls with M <=
+// max_M allocate and compile nothing, so they can be captured in a graph.
 extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
 {
     if (!h || max_M < 0) return fail(TSG_ERR_ARG, "bad reserve arguments");
     DeviceGuard g(h->device);
-    int rc = ensure_work(h, max_M);
+    std::lock_guard<std::mutex> lk(h->mu);
+    int rc = ensure_work(h, max_M, false);
     if (rc || h->kind != tsg_tcsc::kJit) return rc;
-    std::lock_guard<std::mutex> lk(h->mu);  // the image a call with max_M rows runs, compiled now
-    return ensure_jit_variant(h, pick_jit_width(h, max_M));
+    const int mtiles = (std::max(max_M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM;
+    for (int mt = 1; mt <= mtiles; mt++) {
+        rc = ensure_jit_variant(h, pick_jit_width(h, std::min(max_M, mt * tsg::kJitTileM)));
+        if (rc) return rc;
+    }
+    return TSG_OK;
 }
 
 extern "C" int tcsc_hip_set_jit_width(tsg_tcsc *h, int width)
@@ -688,30 +708,21 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     o->nnz_neg = h->nnz_neg;
     // TCSC / BlockedTCSC getDataStructureSize (TCSC.h:43-49, BlockedTCSC.h:43-47)
     o->tcsc_bytes = 4 * (2 * (int64_t)h->csp.size() + h->nnz_pos + h->nnz_neg);
-    const bool rx = h->kind == tsg_tcsc::kRx || h->kind == tsg_tcsc::kJit;
+    const bool jit = h->kind == tsg_tcsc::kJit;
     int64_t jit_bytes = 0;
     for (const auto &v : h->jv) jit_bytes += v.code_bytes + v.wcode_words * 4;
-    o->image_bytes = h->kind == tsg_tcsc::kJit ? jit_bytes
-                     : rx ? (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4
-                     : h->stream_kernel ? (int64_t)(h->simg.wstart.size() + h->simg.ent.size()) * 4
-                                        : (int64_t)(h->img.seg.size() + h->img.ent.size()) * 4;
+    o->image_bytes = jit ? jit_bytes : (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;
-    const bool jit = h->kind == tsg_tcsc::kJit;
-    o->chunk_rows = jit ? tsg::kJitChunk : rx ? tsg::kRxChunk : h->stream_kernel ? tsg::kSChunk : tsg::kChunkK;
-    o->tile_rows = jit ? tsg::kJitTileM : rx ? tsg::kRxTileM : tsg::kTileM;
-    o->tile_cols = jit ? tsg::kJitTileCols : rx ? tsg::kRxTileCols : h->stream_kernel ? h->simg.tile_cols : h->img.tile_cols;
+    o->chunk_rows = jit ? tsg::kJitChunk : tsg::kRxChunk;
+    o->tile_rows = jit ? tsg::kJitTileM : tsg::kRxTileM;
+    o->tile_cols = jit ? tsg::kJitTileCols : tsg::kRxTileCols;
     return TSG_OK;
 }
 
 extern "C" const char *tcsc_hip_kernel_name(const tsg_tcsc *h)
 {
     if (!h) return "";
-    switch (h->kind) {
-    case tsg_tcsc::kJit: return "tsg_jit_kernel";
-    case tsg_tcsc::kRx: return "tsg_tcsc_rx_kernel";
-    case tsg_tcsc::kStream: return "tsg_tcsc_stream_kernel";
-    default: return "tsg_tcsc_lds_kernel";
-    }
+    return h->kind == tsg_tcsc::kJit ? "tsg_jit_kernel" : "tsg_tcsc_rx_kernel";
 }
 
 extern "C" int tcsc_hip_to_dense(const tsg_tcsc *h, int32_t *W, int K, int N)

@@ -13,165 +13,6 @@
 
 namespace tsg {
 
-int pick_tile_cols(int N)
-{
-    // kWaves waves x NW columns.  NW = 32 (64 accumulator VGPRs) unless N is
-    // so small that most of a 128-column tile would be padding.
-    return N <= 64 ? kWaves * 16 : kWaves * 32;
-}
-
-void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                 const int32_t *rin, int K, int N, int tile_cols, Image &img)
-{
-    img.K = K;
-    img.N = N;
-    img.tile_cols = tile_cols;
-    img.Npad = ((N + tile_cols - 1) / tile_cols) * tile_cols;
-    img.nch = std::max(1, (K + kChunkK - 1) / kChunkK);
-    const int nch = img.nch;
-    img.seg.assign((size_t)img.Npad * 2 * (nch + 1), 0u);
-    img.ent.clear();
-    const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
-    img.ent.reserve((size_t)(nnz / kEntPerWord) + (size_t)img.Npad * 2 * nch + 64);
-
-    for (int n = 0; n < img.Npad; n++) {
-        for (int p = 0; p < 2; p++) {
-            const int32_t *cs = p ? csn : csp;
-            const int32_t *ri = p ? rin : rip;
-            int32_t i = n < N ? cs[n] : 0;
-            const int32_t e = n < N ? cs[n + 1] : 0;
-            uint32_t *seg = &img.seg[((size_t)n * 2 + p) * (nch + 1)];
-            for (int j = 0; j < nch; j++) {
-                seg[j] = (uint32_t)img.ent.size();
-                const int32_t khi = (j + 1) * kChunkK;
-                uint32_t word = 0;
-                int fill = 0;
-                while (i < e && ri[i] < khi) {
-                    word |= (uint32_t)(ri[i] - j * kChunkK) << (8 * fill);
-                    if (++fill == kEntPerWord) {
-                        img.ent.push_back(word);
-                        word = 0;
-                        fill = 0;
-                    }
-                    i++;
-                }
-                if (fill) {  // pad the last group with the +0.0f row
-                    for (; fill < kEntPerWord; fill++) word |= (uint32_t)kZeroRow << (8 * fill);
-                    img.ent.push_back(word);
-                }
-            }
-            seg[nch] = (uint32_t)img.ent.size();
-        }
-    }
-    img.ent.resize(img.ent.size() + 64, 0u);  // tail: keeps any over-fetch in bounds
-}
-
-int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, int nw, bool flat, StreamImage &img)
-{
-    img.K = K;
-    img.N = N;
-    img.nw = nw;
-    img.flat = flat;
-    img.tile_cols = kSWaves * nw;
-    img.Npad = ((N + img.tile_cols - 1) / img.tile_cols) * img.tile_cols;
-    img.nch = std::max(1, (K + kSChunk - 1) / kSChunk);
-    const int nch = img.nch, ntiles = img.Npad / img.tile_cols;
-    const int hdr_words = flat ? kSFlatHdrWords : ((1 + nw / kEntPerWord) + 1) & ~1;
-    img.wstart.assign((size_t)ntiles * kSWaves, 0u);
-    img.ent.clear();
-    const int64_t nnz = (int64_t)csp[N] + (int64_t)csn[N];
-    img.ent.reserve((size_t)(nnz / kEntPerWord) * 5 / 4 + (size_t)img.Npad * 2 * nch * 2 + 512);
-    int maxsub = 0;
-
-    auto align = [&](size_t a) { while (img.ent.size() % a) img.ent.push_back(0u); };
-    std::vector<int32_t> cur((size_t)nw * 2);  // per column & pass: next row index
-    for (int t = 0; t < ntiles; t++) {
-        for (int w = 0; w < kSWaves; w++) {
-            const int n0 = t * img.tile_cols + w * nw;
-            align(4);
-            img.wstart[(size_t)t * kSWaves + w] = (uint32_t)img.ent.size();
-            for (int c = 0; c < nw; c++)
-                for (int p = 0; p < 2; p++) {
-                    const int n = n0 + c;
-                    cur[(size_t)c * 2 + p] = n < N ? (p ? csn[n] : csp[n]) : 0;
-                }
-            for (int q = 0; q < 2 * nch; q++) {
-                const int p = q / nch, j = q % nch;
-                const uint32_t par = (uint32_t)(q & 1) << 7;
-                const int32_t *cs = p ? csn : csp;
-                const int32_t *ri = p ? rin : rip;
-                align(4);  // sub-stream: 16-byte aligned for the LDS-DMA piece
-                const size_t sub0 = img.ent.size();
-                img.ent.resize(sub0 + hdr_words, 0u);
-                int last_nonempty = -1;
-                for (int c = 0; c < nw; c++) {
-                    if (!flat) align(2);  // segment: 8-byte aligned for ds_read_b64
-                    const size_t seg0 = img.ent.size();
-                    const int n = n0 + c;
-                    int32_t &i = cur[(size_t)c * 2 + p];
-                    const int32_t e = n < N ? cs[n + 1] : 0;
-                    const int32_t khi = (j + 1) * kSChunk;
-                    uint32_t word = 0, nent = 0;
-                    int fill = 0;
-                    while (i < e && ri[i] < khi) {
-                        nent++;
-                        word |= ((uint32_t)(ri[i] - j * kSChunk) | par) << (8 * fill);
-                        if (++fill == kEntPerWord) {
-                            img.ent.push_back(word);
-                            word = 0;
-                            fill = 0;
-                        }
-                        i++;
-                    }
-                    if (fill) {  // pad the last group with the +0.0f row of this buffer
-                        for (; fill < kEntPerWord; fill++)
-                            word |= ((uint32_t)kSZeroRow | par) << (8 * fill);
-                        img.ent.push_back(word);
-                    }
-                    if (flat) {  // dwords of the segment; segments follow each other
-                        const uint32_t dw = (uint32_t)(img.ent.size() - seg0);
-                        img.ent[sub0 + 2 + c / kEntPerWord] |= dw << (8 * (c % kEntPerWord));
-                        if (dw) last_nonempty = c;
-                    } else {  // exact entry count (<= kSChunk)
-                        img.ent[sub0 + 1 + c / kEntPerWord] |= nent << (8 * (c % kEntPerWord));
-                    }
-                }
-                if (flat) {
-                    size_t D = img.ent.size() - sub0 - hdr_words;
-                    // D a multiple of 4: the kernel's pipeline walks index
-                    // batches of 4 dwords; the extra dwords of +0.0f-row
-                    // entries join the last non-empty segment
-                    while (D & 3) {
-                        img.ent.push_back(0x01010101u * ((uint32_t)kSZeroRow | par));
-                        const int c = last_nonempty;
-                        img.ent[sub0 + 2 + c / kEntPerWord] += 1u << (8 * (c % kEntPerWord));
-                        D++;
-                    }
-                    img.ent[sub0 + 1] = (uint32_t)D;
-                }
-                align(4);  // len is the exact distance to the next sub-stream
-                const size_t len = img.ent.size() - sub0;
-                img.ent[sub0] = (uint32_t)len;
-                maxsub = std::max(maxsub, (int)len);
-            }
-        }
-    }
-    align(4);
-    img.ent.resize(img.ent.size() + kSSubMax + 64, 0u);  // a 1 KiB DMA piece may run past the end
-    return maxsub;
-}
-
-void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, bool flat, StreamImage &img)
-{
-    for (int nw : {16, 8}) {
-        if (nw == 16 && N <= kSWaves * 8) continue;  // tiny N: narrower tiles waste less
-        if (build_stream_image(csp, csn, rip, rin, K, N, nw, flat, img) <= kSSubMax) return;
-    }
-    build_stream_image(csp, csn, rip, rin, K, N, 4, flat, img);  // 8 + 4*32+1 dwords always fit
-}
-
 void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                     const int32_t *rin, int K, int N, RxImage &img)
 {

@@ -10,57 +10,6 @@
 namespace tsg {
 
 constexpr int kLanes = 64;                     // wavefront width (CDNA)
-constexpr int kRowsPerLane = 2;                // M rows one lane accumulates (float2 = ds_read_b64)
-constexpr int kTileM = kLanes * kRowsPerLane;  // 128 M rows per workgroup
-constexpr int kEntPerWord = 4;                 // uint8 entries per dword
-
-// ---------------------------------------------------------------------------
-// "stream" kernel (tsg_tcsc_stream_kernel, the default)
-//
-// LDS image of one X^T chunk, double buffered, 128 KiB:
-//   byte(buf, half, row, l) = half*65536 + buf*32768 + row*256 + l*8
-// with lane = 32*half + l owning M rows m0 + 2*lane + {0,1}.  An entry byte
-// e = row | buf<<7 is byte 1 of that address, the lane constant supplies
-// bytes 0 and 2, so ONE v_perm_b32 turns a packed entry into the ds_read_b64
-// address (no scalar ALU per entry).  Row kZeroRow of each buffer holds +0.0f.
-constexpr int kSChunk = 127;        // K rows per chunk (row 127 = zero row)
-constexpr int kSZeroRow = 127;
-constexpr int kSWaves = 16;         // waves per workgroup (1024 threads, 1 WG per CU)
-constexpr int kSLdsBytes = 131072;     // X^T double buffer
-constexpr int kSIdxWaveBytes = 1024;   // per wave per buffer: 256 dwords of entry stream
-constexpr int kSIdxBytes = kSWaves * 2 * kSIdxWaveBytes;  // 32 KiB -> 160 KiB in all
-constexpr int kSSubMax = kSIdxWaveBytes / 4;             // max dwords of one step's sub-stream
-
-// Entry stream of one wave: for every chunk step q = p*nch + j (p = 0: the
-// +1 runs over all K chunks, then p = 1: the -1 runs) a sub-stream starting
-// on a 16-byte boundary: header [total dwords of the sub-stream][NW count
-// bytes = entries of each column segment] padded to an even length, then the
-// NW segments (each starting on an even dword): entries
-// (k - j*kSChunk) | (q&1)<<7, ascending k, 4 per dword, the last dword padded
-// with kSZeroRow | (q&1)<<7.  A sub-stream is at most kSSubMax dwords; the
-// planner lowers nw (16 -> 8 -> 4) until that holds.
-// Flat variant (default, tsg_tcsc_flat_kernel): the header is 8 dwords
-// [len][D = data dwords, even][NW bytes = dwords of each column segment]...,
-// data at +32 B, segments back to back (no per-segment alignment), every
-// segment padded to whole dwords with +0.0f-row entries, and one more such
-// dword appended to the last non-empty segment when D would be odd.
-constexpr int kSFlatHdrWords = 8;
-
-struct StreamImage {
-    int K = 0, N = 0, Npad = 0, nch = 0;
-    bool flat = true;
-    int nw = 0;                     // columns per wave
-    int tile_cols = 0;              // kSWaves * nw
-    std::vector<uint32_t> wstart;   // per (column tile, wave): first dword of its stream
-    std::vector<uint32_t> ent;      // all streams (+ tail padding)
-};
-// Returns the largest sub-stream (dwords); callers retry with a smaller nw
-// when it exceeds kSSubMax.
-int build_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, int nw, bool flat, StreamImage &img);
-// Builds with the widest nw (16, 8, 4) whose sub-streams fit.
-void plan_stream_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                       const int32_t *rin, int K, int N, bool flat, StreamImage &img);
 
 // ---------------------------------------------------------------------------
 // "rx" (register-X) kernel (tsg_tcsc_rx_kernel)
@@ -173,22 +122,6 @@ int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                     int prelu, uint32_t *status, int tile_cols, void *stream);
 
-// ---------------------------------------------------------------------------
-// "chunked" kernel (tsg_tcsc_lds_kernel, round-1 v1, kept for A/B)
-constexpr int kChunkK = 128;        // K rows of X^T staged in LDS per chunk
-constexpr int kZeroRow = kChunkK;   // LDS row holding +0.0f (pads index groups)
-constexpr int kWaves = 4;           // waves per workgroup (256 threads)
-
-struct Image {
-    int K = 0, N = 0, Npad = 0, nch = 0;
-    int tile_cols = 0;
-    std::vector<uint32_t> seg;   // Npad * 2 * (nch + 1)
-    std::vector<uint32_t> ent;   // packed entries (+ tail padding)
-};
-void build_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                 const int32_t *rin, int K, int N, int tile_cols, Image &img);
-int pick_tile_cols(int N);
-
 // B = 0: plain TCSC; B > 0: BlockedTCSC<B> arrays ((K/B)*N + 1 column starts)
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                           const int32_t *rin, int K, int N, int B = 0);
@@ -203,15 +136,8 @@ int encode_fill(const int32_t *dW, int K, int N, const int32_t *d_csp, const int
 
 // Kernel launchers (csrc/tcsc_kernels.hip).  All enqueue on `stream`.
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream);
-int launch_tcsc(const float *XT, int Mp, const uint32_t *seg, const uint32_t *ent,
-                const float *b, const float *alpha, float *Y, int M, int N, int Npad,
-                int nch, int tile_cols, int prelu, void *stream);
-int launch_tcsc_stream(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
-                       const float *zero, const float *b, const float *alpha, float *Y, int M,
-                       int N, int Npad, int nch, int nw, int prelu, unsigned long long *stamps,
-                       bool flat, void *stream);
 int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                    const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
-                   int prelu, unsigned long long *stamps, void *stream);
+                   int prelu, void *stream);
 
 }  // namespace tsg

@@ -218,6 +218,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     uint32_t touch_first = 1, touch_count = 1;
     if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
     if (touch_count > 4) touch_count = 4;
+    // the prefetch must stay inside the tail padding past the last stream
+    if ((touch_first + touch_count) * 8192u > (uint32_t)kTailPad * 4u) touch_first = (uint32_t)kTailPad * 4u / 8192u - touch_count;
     const uint32_t ntouch = d_notouch ? 0u : touch_count;
 
     int n0 = 0;  // first column of the current stream
@@ -414,6 +416,7 @@ namespace {
 std::string template_path(int nw)
 {
     const std::string name = nw == kJitNW ? "tsg_jit.co" : "tsg_jit_w" + std::to_string(nw) + ".co";
+    if (const char *dir = std::getenv("TSG_JIT_DIR")) return std::string(dir) + "/" + name;  // tests: rx fallback
     Dl_info info;
     if (dladdr(reinterpret_cast<void *>(&build_jit_code), &info) && info.dli_fname) {
         std::string p(info.dli_fname);

@@ -145,6 +145,12 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
         if (blockIdx.x == 0 && tid == 0) status[0] = 1u;
         return;
     }
+    // probe launch (tsg_capi.cpp ensure_jit_variant, once per loaded image):
+    // the region was found; report it and run nothing else
+    if (prelu & 2) {
+        if (blockIdx.x == 0 && tid == 0) status[1] = kJMagic0;
+        return;
+    }
 
     // XCD-aware bijective remap: each XCD gets a contiguous run of workgroup
     // ids (blocks b and b+8 share an XCD), and consecutive ids walk groups of
@@ -279,7 +285,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
             if (prelu) y = (y > 0) ? y : alpha[n] * y;   // comp_prelu.h:57-67
             v[c] = y;
         }
-        if (ncol0 + kJNW <= N && ((((size_t)m * N + ncol0) & 3) == 0)) {
+        if (ncol0 + kJNW <= N && (((uintptr_t)yrow & 15) == 0)) {  // float4 stores need 16-B alignment
 #pragma unroll
             for (int c = 0; c < kJNW; c += 4)
                 *reinterpret_cast<float4 *>(yrow + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);

@@ -358,6 +358,13 @@ class TCSCDevice:
         return cls(csp.cpu().numpy(), csn.cpu().numpy(), rip.cpu().numpy(), rin.cpu().numpy(), K, N,
                    device=W.device.index if device < 0 else device)
 
+    @property
+    def device(self) -> int:
+        """HIP device index the handle's image lives on (tcsc_hip_info)."""
+        if getattr(self, "_device", None) is None:
+            self._device = int(self.info()["device"])
+        return self._device
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             lib().tcsc_hip_destroy(self._h)
@@ -376,11 +383,25 @@ class TCSCDevice:
         self.close()
 
     # ---- comp_func surface (host pointers, synchronous) ----
+    def _check_host(self, M: int, N: int, K: int, **arrays) -> None:
+        """Host-pointer call contract (main.cpp:214-216): fp32, C-contiguous,
+        X holds M*K floats, Y M*N, B (and alpha) N -- checked before the C-ABI
+        sees the pointers, so a short buffer raises instead of being overrun."""
+        if (N, K) != (self.N, self.K):
+            return  # the C-ABI reports the shape mismatch (TSG_ERR_ARG)
+        need = {"X": M * K, "B": N, "Y": M * N, "alpha": N}
+        for name, a in arrays.items():
+            if not isinstance(a, np.ndarray) or a.dtype != np.float32 or not a.flags.c_contiguous:
+                raise TSGError(1, "comp_func", f"{name} must be a C-contiguous float32 numpy array")
+            if a.size < need[name]:
+                raise TSGError(1, "comp_func", f"{name} has {a.size} floats, the call needs {need[name]}")
+        X = arrays.get("X")
+        if X is not None and X.ndim == 2 and X.shape[1] != K:
+            raise TSGError(1, "comp_func", f"X is {X.shape}, rows must have K={K} floats")
+
     def __call__(self, X, B, Y, M: int, N: int, K: int) -> None:
         """comp_func(X, B, Y, M, N, K) on numpy arrays (common.h:12)."""
-        assert X.dtype == np.float32 and B.dtype == np.float32 and Y.dtype == np.float32
-        assert X.flags.c_contiguous and Y.flags.c_contiguous and B.flags.c_contiguous
-        assert X.size >= M * K and B.size >= N and Y.size >= M * N
+        self._check_host(M, N, K, X=X, B=B, Y=Y)
         _check(lib().tcsc_hip_gemm(self._h, X.ctypes.data, B.ctypes.data, Y.ctypes.data, M, N, K),
                "tcsc_hip_gemm")
 
@@ -389,6 +410,7 @@ class TCSCDevice:
 
     def prelu(self, X, B, alpha, Y, M: int, N: int, K: int) -> None:
         """comp_func_prelu(X, B, alpha, Y, M, N, K) (common.h:13)."""
+        self._check_host(M, N, K, X=X, B=B, alpha=alpha, Y=Y)
         _check(lib().tcsc_hip_gemm_prelu(self._h, X.ctypes.data, B.ctypes.data, alpha.ctypes.data,
                                          Y.ctypes.data, M, N, K), "tcsc_hip_gemm_prelu")
 
@@ -417,13 +439,27 @@ class TCSCDevice:
                                                  stream or None), "tcsc_hip_gemm_prelu_dev")
 
     def gemm_torch(self, X, b, Y=None, alpha=None):
-        """X [M,K] fp32 cuda tensor -> Y [M,N], enqueued on torch's current stream."""
+        """X [M,K] fp32 cuda tensor -> Y [M,N], enqueued on torch's current stream.
+        Every tensor must be float32, contiguous and on the handle's device;
+        shapes X (M, K), b (N,), alpha (N,), Y (M, N) are checked here (the
+        C-ABI only sees raw pointers)."""
         import torch
-        assert X.is_cuda and X.dtype == torch.float32 and X.is_contiguous()
+        dev = torch.device("cuda", self.device)
+        if not (isinstance(X, torch.Tensor) and X.dim() == 2 and X.shape[1] == self.K):
+            raise TSGError(1, "gemm_torch", f"X must be a [M, {self.K}] tensor, got "
+                                            f"{tuple(X.shape) if isinstance(X, torch.Tensor) else type(X)}")
         M = X.shape[0]
         if Y is None:
-            Y = torch.empty((M, self.N), dtype=torch.float32, device=X.device)
-        stream = torch.cuda.current_stream(X.device).cuda_stream
+            Y = torch.empty((M, self.N), dtype=torch.float32, device=dev)
+        for name, t, shape in (("X", X, (M, self.K)), ("b", b, (self.N,)), ("Y", Y, (M, self.N)),
+                               ("alpha", alpha, (self.N,))):
+            if t is None:
+                continue
+            if t.dtype != torch.float32 or t.device != dev or not t.is_contiguous() or tuple(t.shape) != shape:
+                raise TSGError(1, "gemm_torch", f"{name} must be a contiguous float32 {list(shape)} tensor on "
+                                                f"{dev}, got {t.dtype} {list(t.shape)} on {t.device}"
+                                                f"{'' if t.is_contiguous() else ' (non-contiguous)'}")
+        stream = torch.cuda.current_stream(dev).cuda_stream
         self.gemm_dev(X.data_ptr(), b.data_ptr(), Y.data_ptr(), M, stream,
                       None if alpha is None else alpha.data_ptr())
         return Y

@@ -149,14 +149,53 @@ def hashed_configs():
                            "sha256_tcsc": sha(np.concatenate(t.arrays)),
                            "sha256_Y_rows": sha(Ys)}
     print("config3 rows done")
+    res.update(sweep_configs())
     with open(os.path.join(HERE, "ref_hashes.json"), "w") as f:
         json.dump(res, f, indent=1)
+
+
+SWEEP_ROWS = [0, 1, 127, 128, 2047, 2048, 4094, 4095]
+
+
+def sweep_configs():
+    """BASELINE.json configs[3]: M=4096 K=4096 N=16384 at s in {2, 8, 16} (s=4 is
+    config3_rows above), sampled rows.  Y from the reference's dense GEMM
+    (sparseUtils.h:92-108), cross-checked against the restatement; the TCSC
+    hash pins the generator, the CSC+packed hash pins tsg_tcsc_to_csc_packed."""
+    out = {}
+    M, K, N, sw, sx = 4096, 4096, 16384, 42, 12345
+    rows = np.array(SWEEP_ROWS, np.int64)
+    X = O.init_x_int(M, K, sx)
+    b = np.full(N, 2.0, np.float32)
+    for s in (2, 8, 16):
+        W = O.gen_ternary(K, N, s, sw)
+        Ys = O.ref_gemm(np.ascontiguousarray(X[rows]), W, b)
+        t = O.tcsc_encode(W)
+        Yo = O.base_tcsc(np.ascontiguousarray(X[rows]), t, b)
+        assert np.array_equal(Ys, Yo), f"restatement disagrees with the reference GEMM at s={s}"
+        cp, ri, pk = O.csc_packed_encode(W)
+        out[f"config4_s{s}_rows"] = {"M": M, "K": K, "N": N, "s": s, "seed_w": sw, "seed_x": sx,
+                                     "rows": rows.tolist(),
+                                     "nnz_pos": int(len(t.row_index_pos)), "nnz_neg": int(len(t.row_index_neg)),
+                                     "sha256_tcsc": sha(np.concatenate(t.arrays)),
+                                     "sha256_csc_packed": sha(np.concatenate([cp.view(np.uint8), ri.view(np.uint8),
+                                                                              pk])),
+                                     "sha256_Y_rows": sha(Ys)}
+        print(f"config4 s={s} rows done")
+    return out
 
 
 if __name__ == "__main__":
     O.build(ref=True)
     assert O.ref_available(), "oracle/_ref/libref.so missing: needs /root/reference"
-    kat_files()
-    small_cases()
-    if "--no-hash" not in sys.argv:
+    if "--sweep-only" not in sys.argv:
+        kat_files()
+        small_cases()
+    if "--sweep-only" in sys.argv:  # add the configs[3] rows to the committed ref_hashes.json
+        path = os.path.join(HERE, "ref_hashes.json")
+        res = json.load(open(path))
+        res.update(sweep_configs())
+        with open(path, "w") as f:
+            json.dump(res, f, indent=1)
+    elif "--no-hash" not in sys.argv:
         hashed_configs()

@@ -249,21 +249,41 @@ def test_default_is_weight_compiled(tsg, oracle_mod):
     assert h.kernel_name() == "tsg_jit_kernel"
 
 
-@pytest.mark.parametrize("family,kernel", [("rx", "tsg_tcsc_rx_kernel"), ("stream", "tsg_tcsc_stream_kernel"),
-                                           ("flat", "tsg_tcsc_stream_kernel")])
-def test_other_kernel_families(tsg, oracle_mod, monkeypatch, family, kernel):
-    """The register-X and LDS-gather kernels (TSG_KERNEL at registration) stay
-    bit-exact too: they are the A/B baselines of DESIGN.md 9."""
-    monkeypatch.setenv("TSG_KERNEL", family)
+def test_rx_kernel_family(tsg, oracle_mod, monkeypatch):
+    """The register-X kernel (TSG_KERNEL=rx at registration; also the fallback
+    for W too large for one compiled image) stays bit-exact too."""
+    monkeypatch.setenv("TSG_KERNEL", "rx")
     O = oracle_mod
     for M, K, N, s in [(129, 257, 65, 4), (300, 1000, 129, 16), (5, 1100, 300, 2)]:
         t = O.tcsc_encode(O.gen_ternary(K, N, s, M + K))
         h = tsg.TCSCDevice(*t.arrays, K, N)
-        assert h.kernel_name() == kernel
+        assert h.kernel_name() == "tsg_tcsc_rx_kernel"
         b = np.linspace(-1, 1, N).astype(np.float32)
+        alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
         X = O.init_x_frac(M, K, 3)
         assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+        assert _bits_eq(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
         h.close()
+
+
+def test_failed_image_load_falls_back_to_rx(tsg, oracle_mod, monkeypatch, capfd):
+    """A weight-compiled image the loader cannot build (here: its dispatcher
+    template is missing) registers on the rx kernel with a logged warning,
+    instead of failing the registration; asking for jit explicitly still fails."""
+    O = oracle_mod
+    monkeypatch.setenv("TSG_JIT_DIR", "/nonexistent-tsg-jit-dir")
+    K, N, M = 300, 200, 70
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 5))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    assert h.kernel_name() == "tsg_tcsc_rx_kernel"
+    assert "falling back to the rx kernel" in capfd.readouterr().err
+    X = O.init_x_frac(M, K, 4)
+    b = np.linspace(-1, 1, N).astype(np.float32)
+    assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+    h.close()
+    monkeypatch.setenv("TSG_KERNEL", "jit")
+    with pytest.raises(tsg.TSGError, match="cannot open jit template"):
+        tsg.TCSCDevice(*t.arrays, K, N)
 
 
 def test_gpu_encoder_matches_host_ctor(tsg, oracle_mod):

@@ -1,0 +1,169 @@
+"""Device-pointer API contract on the GPU (include/ternary_spgemm.h,
+tcsc_hip_gemm_dev): several streams / threads on one handle, graph capture
+after tcsc_hip_reserve, and the argument checks of the Python mirror."""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def test_two_streams_one_handle(tsg, oracle_mod):
+    """Calls on two streams with different X, issued back to back without a
+    host sync: each call's X^T staging must wait for the other stream's kernel
+    (shared work buffer), so both results stay bit-exact."""
+    import torch
+    O = oracle_mod
+    K, N, M = 2048, 4096, 1024
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 21))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.reserve(M)
+    b = torch.from_numpy(np.linspace(-1, 1, N).astype(np.float32)).cuda()
+    X1n, X2n = O.init_x_frac(M, K, 1), O.init_x_frac(M, K, 2)
+    X1, X2 = torch.from_numpy(X1n).cuda(), torch.from_numpy(X2n).cuda()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(4):
+        with torch.cuda.stream(s1):
+            Y1 = h.gemm_torch(X1, b)
+        with torch.cuda.stream(s2):
+            Y2 = h.gemm_torch(X2, b)
+        outs.append((Y1, Y2))
+    torch.cuda.synchronize()
+    rows = np.r_[0:64, M - 64:M]
+    bn = b.cpu().numpy()
+    r1 = O.base_tcsc(np.ascontiguousarray(X1n[rows]), t, bn)
+    r2 = O.base_tcsc(np.ascontiguousarray(X2n[rows]), t, bn)
+    for Y1, Y2 in outs:
+        assert np.array_equal(_bits(Y1)[rows], r1.view(np.uint32))
+        assert np.array_equal(_bits(Y2)[rows], r2.view(np.uint32))
+        assert torch.equal(Y1.view(torch.int32), outs[0][0].view(torch.int32))
+        assert torch.equal(Y2.view(torch.int32), outs[0][1].view(torch.int32))
+    h.close()
+
+
+def test_threads_one_handle(tsg, oracle_mod):
+    """Two host threads, each on its own stream, share one handle."""
+    import torch
+    O = oracle_mod
+    K, N, M = 1000, 1500, 300
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 22))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    b = torch.full((N,), 2.0, device="cuda")
+    Xs = [O.init_x_frac(M, K, 10 + i) for i in range(2)]
+    res = [None, None]
+
+    def work(i):
+        torch.cuda.set_device(0)
+        s = torch.cuda.Stream()
+        X = torch.from_numpy(Xs[i]).cuda()
+        with torch.cuda.stream(s):
+            for _ in range(5):
+                Y = h.gemm_torch(X, b)
+        s.synchronize()
+        res[i] = Y.cpu().numpy()
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    bn = np.full(N, 2.0, np.float32)
+    for i in range(2):
+        assert np.array_equal(res[i].view(np.uint32), O.base_tcsc(Xs[i], t, bn).view(np.uint32))
+    h.close()
+
+
+@pytest.mark.parametrize("M", [4096, 96])
+def test_graph_capture_after_reserve(tsg, oracle_mod, M):
+    """tcsc_hip_reserve(max_M) prepares every width a call with M <= max_M runs;
+    the call is then captured into a HIP graph (no allocation, compile or sync
+    inside) and each replay recomputes Y from the current X."""
+    import torch
+    O = oracle_mod
+    K, N = 1024, 2048
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 23))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.reserve(4096)
+    b = torch.full((N,), 2.0, device="cuda")
+    Xs = torch.zeros((M, K), device="cuda")
+    Ys = torch.empty((M, N), device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up outside capture
+        h.gemm_torch(Xs, b, Ys)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        h.gemm_torch(Xs, b, Ys)
+    bn = np.full(N, 2.0, np.float32)
+    for seed in (1, 2):
+        Xn = O.init_x_frac(M, K, seed)
+        Xs.copy_(torch.from_numpy(Xn).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        rows = np.r_[0:16, M - 16:M]
+        ref = O.base_tcsc(np.ascontiguousarray(Xn[rows]), t, bn)
+        assert np.array_equal(_bits(Ys)[rows], ref.view(np.uint32)), seed
+    h.close()
+
+
+def test_capture_without_reserve_fails_loudly(tsg, oracle_mod):
+    """A call that would have to grow the work buffer inside a capture is refused
+    with TSG_ERR_ARG (and a hint), instead of breaking the capture."""
+    import torch
+    O = oracle_mod
+    K, N = 500, 300
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 24))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    b = torch.full((N,), 2.0, device="cuda")
+    X = torch.zeros((2000, K), device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(tsg.TSGError, match="tcsc_hip_reserve"):
+        with torch.cuda.graph(g):
+            h.gemm_torch(X, b)
+    torch.cuda.synchronize()
+    h.close()
+
+
+def test_torch_argument_checks(tsg, oracle_mod):
+    """gemm_torch refuses tensors the raw-pointer C-ABI would misread."""
+    import torch
+    O = oracle_mod
+    K, N, M = 64, 48, 8
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 25))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    X = torch.zeros((M, K), device="cuda")
+    b = torch.zeros(N, device="cuda")
+    Ybig = torch.zeros((M, 2 * N), device="cuda")
+    bad = [
+        dict(X=torch.zeros((M, K - 1), device="cuda"), b=b),            # narrow X
+        dict(X=X, b=torch.zeros(N - 1, device="cuda")),                 # short b
+        dict(X=X, b=b, Y=Ybig[:, :N]),                                   # non-contiguous Y
+        dict(X=X, b=b, Y=torch.zeros((M, N + 1), device="cuda")),       # wrong Y shape
+        dict(X=X.double(), b=b),                                         # dtype
+        dict(X=X, b=b.cpu()),                                            # device
+        dict(X=X, b=b, alpha=torch.zeros(N - 2, device="cuda")),        # short alpha
+    ]
+    for kw in bad:
+        with pytest.raises(tsg.TSGError):
+            h.gemm_torch(**kw)
+    with pytest.raises(tsg.TSGError):
+        h(np.zeros((M, K - 1), np.float32), np.zeros(N, np.float32), np.zeros((M, N), np.float32), M, N, K)
+    with pytest.raises(tsg.TSGError):
+        h(np.zeros((M, K), np.float32), np.zeros(N - 1, np.float32), np.zeros((M, N), np.float32), M, N, K)
+    # Y with a storage offset that breaks 16-byte alignment still gets correct
+    # values (the kernel's float4 stores check the pointer)
+    Yo = torch.zeros(M * N + 1, device="cuda")[1:].view(M, N)
+    Xn = O.init_x_frac(M, K, 3)
+    h.gemm_torch(torch.from_numpy(Xn).cuda(), b, Y=Yo)
+    torch.cuda.synchronize()
+    assert np.array_equal(_bits(Yo), O.base_tcsc(Xn, t, np.zeros(N, np.float32)).view(np.uint32))
+    h.close()

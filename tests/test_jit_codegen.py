@@ -11,6 +11,9 @@ read-after-DMA race) while no DMA may overwrite rows read since it was issued
 The emulated Y must equal the BaseTCSC oracle (comp.h:25-69) bit for bit, for
 integer and for order-sensitive non-integer X.  tests/test_gpu_parity.py then
 shows the GPU runs that code."""
+import os
+import struct
+
 import numpy as np
 import pytest
 
@@ -338,7 +341,6 @@ def test_jit_code_emulates_base_blocked_tcsc(tsg, oracle_mod, M, K, N, s, B):
 def test_jit_code_blocked_kat(tsg, oracle_mod):
     """The 4x4, B = 2 example of plots/data_example_image/blocked.py:12-30."""
     import json
-    import os
     kat = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kat_blocked_4x4_B2.json")))
     W = np.array(kat["W"], np.int32)
     _check_blocked(tsg, oracle_mod, 4, 4, 4, 0, 2, 1, True, W=W)
@@ -368,3 +370,41 @@ def test_blocked_validation_rejects_malformed(tsg, oracle_mod):
             tsg.validate_blocked(csp, csn, bad, rin, 64, 6, 16)
     with pytest.raises(tsg.TSGError):
         tsg.validate_blocked(csp, csn, rip, rin, 64, 6, 0)
+
+
+# ---------------------------------------------------------------------------
+# Float mode of the shipped dispatchers (no GPU): the generated adds run under
+# the dispatcher's kernel descriptor, which must keep FP32 denormals and IEEE
+# mode for the special-value contract of DESIGN.md section 3
+# (tests/test_gpu_special.py checks the results on the GPU).
+
+_REPO_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _rsrc1_of(co_path, symbol="tsg_jit_kernel.kd"):
+    data = open(co_path, "rb").read()
+    # ELF64: section headers -> .symtab / .strtab -> the .kd symbol's file offset
+    (e_shoff,) = struct.unpack_from("<Q", data, 0x28)
+    e_shentsize, e_shnum = struct.unpack_from("<HH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", data, e_shoff + i * e_shentsize) for i in range(e_shnum)]
+    for sh in secs:
+        if sh[1] == 2:  # SHT_SYMTAB
+            strtab = secs[sh[6]]
+            for j in range(sh[5] // 24):
+                st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from(
+                    "<IBBHQQ", data, sh[4] + j * 24)
+                end = data.index(b"\0", strtab[4] + st_name)
+                if data[strtab[4] + st_name:end].decode() == symbol:
+                    tgt = secs[st_shndx]
+                    off = tgt[4] + (st_value - tgt[3])
+                    (rsrc1,) = struct.unpack_from("<I", data, off + 0x30)
+                    return rsrc1
+    raise AssertionError(f"{symbol} not found in {co_path}")
+
+
+@pytest.mark.parametrize("co", ["tsg_jit.co", "tsg_jit_w32.co", "tsg_jit_w16.co", "tsg_jit_w8.co"])
+def test_kernel_descriptor_float_mode(co):
+    rsrc1 = _rsrc1_of(os.path.join(_REPO_ROOT, "ternary-spgemm_amd", "lib", co))
+    assert (rsrc1 >> 16) & 3 == 3, "FP32 denormals must be preserved (FLOAT_DENORM_MODE_32)"
+    assert (rsrc1 >> 23) & 1 == 1, "IEEE mode must be on"
+
