@@ -59,6 +59,10 @@ def lib() -> C.CDLL:
         L.oracle_base_csc_packed.argtypes = [_f32p, _i32p, _i32p, _u8p, _f32p, _f32p,
                                              C.c_int, C.c_int, C.c_int]
         L.oracle_base_csc_packed.restype = None
+        L.oracle_perf_calibrated.argtypes = [C.c_int, C.c_int, C.c_double, _f32p, _i32p, _i32p, _i32p, _i32p,
+                                             _f32p, _f32p, C.c_int, C.c_int, C.c_int, C.POINTER(_i64),
+                                             C.POINTER(C.c_double)]
+        L.oracle_perf_calibrated.restype = C.c_double
         for f in ("oracle_gen_ternary", "oracle_init_x_int", "oracle_init_x_frac",
                   "oracle_tcsc_count", "oracle_tcsc_encode", "oracle_tcsc_decode",
                   "oracle_blocked_tcsc_encode", "oracle_base_tcsc", "oracle_base_tcsc_omp",
@@ -228,6 +232,23 @@ def double_unrolled_tcsc(X, t: TCSC, b) -> np.ndarray:
     Y = np.empty((M, t.N), dtype=np.float32)
     lib().oracle_double_unrolled_tcsc_k4m4(X, *t.arrays, b, Y, M, t.N, t.K)
     return Y
+
+
+PERF_KERNELS = {"BaseTCSC": 0, "BaseTCSC_omp": 1, "DoubleUnrolledTCSC_K4_M4": 2}
+
+
+def perf_calibrated(kernel: str, X, t: TCSC, b, threads: int = 0, cycles_required: float = 1e8):
+    """The reference's timing method (perf.cpp:37-71, CALIBRATE on): doubles
+    the run count until a batch takes >= 1e8 TSC cycles, then times that many
+    runs.  Returns (seconds per call, runs, TSC cycles per call, Y)."""
+    X, b, M = _prep(X, t, b)
+    Y = np.empty((M, t.N), dtype=np.float32)
+    runs, cyc = _i64(), C.c_double()
+    rip = t.row_index_pos if len(t.row_index_pos) else np.zeros(1, np.int32)
+    rin = t.row_index_neg if len(t.row_index_neg) else np.zeros(1, np.int32)
+    sec = lib().oracle_perf_calibrated(PERF_KERNELS[kernel], threads, cycles_required, X, t.col_start_pos,
+                                       t.col_start_neg, rip, rin, b, Y, M, t.N, t.K, C.byref(runs), C.byref(cyc))
+    return sec, runs.value, cyc.value, Y
 
 
 def base_tcsc_prelu(X, t: TCSC, b, alpha) -> np.ndarray:

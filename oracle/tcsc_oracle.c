@@ -10,8 +10,12 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #ifdef _OPENMP
 #include <omp.h>
+#endif
+#if defined(__x86_64__)
+#include <x86intrin.h>
 #endif
 
 /* ---------------------------------------------------------------- inputs -- */
@@ -364,4 +368,63 @@ void oracle_gemm_dense(const float *X, const float *W, const float *b, float *Y,
             for (int k = 0; k < K; k++) y += X[(size_t)m * K + k] * W[(size_t)k * N + n];
             Y[(size_t)m * N + n] = y + b[n];
         }
+}
+
+/* ------------------------------------------------------------------ timing -- */
+
+/* The reference's measurement method, perf.cpp:37-71 (rdtsc) with CALIBRATE
+ * on (Makefile:11-16): starting at NUM_RUNS = 1 (perf.cpp:28) the run count
+ * doubles until one batch of runs takes >= CYCLES_REQUIRED TSC cycles
+ * (perf.cpp:29, 1e8) or 2^14 runs, then that many runs are timed again and
+ * the average is returned.  Here the TSC is read with __rdtsc() (tsc_x86.h
+ * uses rdtsc behind cpuid serialisation) and the wall-clock seconds of the
+ * timed batch are reported beside the cycles, because the TSC rate of the host
+ * is not known a priori.  kernel: 0 BaseTCSC (comp.h:25-69), 1 BaseTCSC with
+ * OpenMP over rows (`threads`), 2 DoubleUnrolledTCSC<4,4> (comp.h:1227-1438). */
+static uint64_t tsc_now(void)
+{
+#if defined(__x86_64__)
+    return __rdtsc();
+#else
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+#endif
+}
+
+static double wall_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void run_kernel(int kernel, int threads, const float *X, const int32_t *csp, const int32_t *csn,
+                       const int32_t *rip, const int32_t *rin, const float *b, float *Y, int M, int N, int K)
+{
+    if (kernel == 1) oracle_base_tcsc_omp(X, csp, csn, rip, rin, b, Y, M, N, K, threads);
+    else if (kernel == 2) oracle_double_unrolled_tcsc_k4m4(X, csp, csn, rip, rin, b, Y, M, N, K);
+    else oracle_base_tcsc(X, csp, csn, rip, rin, b, Y, M, N, K);
+}
+
+double oracle_perf_calibrated(int kernel, int threads, double cycles_required, const float *X,
+                              const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                              const float *b, float *Y, int M, int N, int K, int64_t *num_runs,
+                              double *cycles_per_run)
+{
+    int64_t runs = 1; /* NUM_RUNS, perf.cpp:28 */
+    while (runs < (1 << 14)) { /* perf.cpp:46-60 */
+        const uint64_t t0 = tsc_now();
+        for (int64_t i = 0; i < runs; i++) run_kernel(kernel, threads, X, csp, csn, rip, rin, b, Y, M, N, K);
+        if ((double)(tsc_now() - t0) >= cycles_required) break;
+        runs *= 2;
+    }
+    const double w0 = wall_now();
+    const uint64_t t0 = tsc_now(); /* perf.cpp:62-69 */
+    for (int64_t i = 0; i < runs; i++) run_kernel(kernel, threads, X, csp, csn, rip, rin, b, Y, M, N, K);
+    const uint64_t cyc = tsc_now() - t0;
+    const double secs = wall_now() - w0;
+    if (num_runs) *num_runs = runs;
+    if (cycles_per_run) *cycles_per_run = (double)cyc / (double)runs;
+    return secs / (double)runs;
 }

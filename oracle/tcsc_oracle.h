@@ -133,6 +133,14 @@ void oracle_base_csc_packed(const float *X, const int32_t *col_ptr, const int32_
 /* Dense GEMM oracle (sparseUtils.h:92-108): y=sum_k X[m,k]*W[k,n]; Y=y+b[n]. */
 void oracle_gemm_dense(const float *X, const float *W, const float *b, float *Y, int M, int N, int K);
 
+/* perf.cpp:37-71 (rdtsc + CALIBRATE): seconds per call of kernel 0 BaseTCSC,
+ * 1 BaseTCSC + OpenMP over rows (threads), 2 DoubleUnrolledTCSC<4,4>; the run
+ * count and TSC cycles per call through the out-pointers. */
+double oracle_perf_calibrated(int kernel, int threads, double cycles_required, const float *X,
+                              const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                              const float *b, float *Y, int M, int N, int K, int64_t *num_runs,
+                              double *cycles_per_run);
+
 #ifdef __cplusplus
 }
 #endif

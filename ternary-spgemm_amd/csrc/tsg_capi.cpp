@@ -256,10 +256,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
         return fail(TSG_ERR_NOMEM, "hipMalloc of the jit status word failed");
     }
     uint32_t st[2] = {0xffffffffu, 0u};
-    const int tile_cols = nw * tsg::kJitStreams;
-    bool ok = hipMemset(h->d_status, 0, 16) == hipSuccess &&
-              tsg::launch_tcsc_jit(v.mod, nullptr, tsg::kJitTileM, v.d_wcode, nullptr, nullptr, nullptr, 0, 0,
-                                   tile_cols, img.nch, 2, h->d_status, tile_cols, nullptr) == 0 &&
+    bool ok = hipMemset(h->d_status, 0, 16) == hipSuccess && tsg::launch_jit_probe(v.mod, h->d_status) == 0 &&
               hipStreamSynchronize(nullptr) == hipSuccess &&
               hipMemcpy(st, h->d_status, sizeof st, hipMemcpyDeviceToHost) == hipSuccess;
     if (!ok || st[0] != 0 || st[1] != tsg::kJitMagic0) {

@@ -115,12 +115,14 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 struct JitModule {
     void *module = nullptr;        // hipModule_t
     void *function = nullptr;      // hipFunction_t of tsg_jit_kernel
+    void *probe = nullptr;         // hipFunction_t of tsg_jit_probe (region check, at load)
     std::string load(const std::vector<uint32_t> &code, int nw = kJitNW);  // "" on success
     void unload();
 };
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                     int prelu, uint32_t *status, int tile_cols, void *stream);
+int launch_jit_probe(const JitModule &jm, uint32_t *status);  // legacy default stream
 
 // B = 0: plain TCSC; B > 0: BlockedTCSC<B> arrays ((K/B)*N + 1 column starts)
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,

@@ -452,25 +452,26 @@ std::string JitModule::load(const std::vector<uint32_t> &code, int nw)
     if (spare < 0) return "jit template has no spare program header";
     const uint64_t page = 0x1000;
     const uint64_t vaddr = (top + page - 1) & ~(page - 1);
-    // patch the dispatcher's literal: s_add_u32 s92, s92, 0x7a5e1234
+    // patch the region-base literal of the dispatcher and of the probe kernel
+    // (each `s_add_u32 s92, s92, 0x7a5e1234` after its own s_getpc_b64): each
+    // becomes (region vaddr - vaddr of that s_add)
     static const unsigned char pat[8] = {0x5c, 0xff, 0x5c, 0x80, 0x34, 0x12, 0x5e, 0x7a};
-    size_t at = std::string::npos;
+    std::vector<size_t> sites;
     for (size_t i = 0; i + 8 <= img.size(); i += 4)
-        if (std::memcmp(img.data() + i, pat, 8) == 0) {
-            if (at != std::string::npos) return "jit template: region literal not unique";
-            at = i;
+        if (std::memcmp(img.data() + i, pat, 8) == 0) sites.push_back(i);
+    if (sites.size() != 2) return "jit template: expected 2 region literals, found " + std::to_string(sites.size());
+    for (const size_t at : sites) {
+        uint64_t insn_vaddr = UINT64_MAX;
+        for (int i = 0; i < eh.e_phnum; i++) {
+            Elf64_Phdr ph;
+            std::memcpy(&ph, img.data() + eh.e_phoff + (size_t)i * sizeof ph, sizeof ph);
+            if (ph.p_type == PT_LOAD && at >= ph.p_offset && at < ph.p_offset + ph.p_filesz)
+                insn_vaddr = ph.p_vaddr + (at - ph.p_offset);
         }
-    if (at == std::string::npos) return "jit template: region literal not found";
-    uint64_t insn_vaddr = UINT64_MAX;
-    for (int i = 0; i < eh.e_phnum; i++) {
-        Elf64_Phdr ph;
-        std::memcpy(&ph, img.data() + eh.e_phoff + (size_t)i * sizeof ph, sizeof ph);
-        if (ph.p_type == PT_LOAD && at >= ph.p_offset && at < ph.p_offset + ph.p_filesz)
-            insn_vaddr = ph.p_vaddr + (at - ph.p_offset);
+        if (insn_vaddr == UINT64_MAX || vaddr - insn_vaddr > 0xffffffffull) return "jit template: bad literal location";
+        const uint32_t lit = (uint32_t)(vaddr - insn_vaddr);
+        std::memcpy(img.data() + at + 4, &lit, 4);
     }
-    if (insn_vaddr == UINT64_MAX || vaddr - insn_vaddr > 0xffffffffull) return "jit template: bad literal location";
-    const uint32_t lit = (uint32_t)(vaddr - insn_vaddr);
-    std::memcpy(img.data() + at + 4, &lit, 4);
     // append the code segment
     const size_t off = (img.size() + page - 1) & ~(size_t)(page - 1);
     const size_t bytes = code.size() * sizeof(uint32_t);
@@ -488,14 +489,16 @@ std::string JitModule::load(const std::vector<uint32_t> &code, int nw)
     hipModule_t m = nullptr;
     hipError_t e = hipModuleLoadData(&m, img.data());
     if (e != hipSuccess) return std::string("hipModuleLoadData: ") + hipGetErrorString(e);
-    hipFunction_t fn = nullptr;
+    hipFunction_t fn = nullptr, pf = nullptr;
     e = hipModuleGetFunction(&fn, m, "tsg_jit_kernel");
+    if (e == hipSuccess) e = hipModuleGetFunction(&pf, m, "tsg_jit_probe");
     if (e != hipSuccess) {
         (void)hipModuleUnload(m);
         return std::string("hipModuleGetFunction: ") + hipGetErrorString(e);
     }
     module = m;
     function = fn;
+    probe = pf;
     return "";
 }
 
@@ -504,6 +507,14 @@ void JitModule::unload()
     if (module) (void)hipModuleUnload((hipModule_t)module);
     module = nullptr;
     function = nullptr;
+    probe = nullptr;
+}
+
+int launch_jit_probe(const JitModule &jm, uint32_t *status)
+{
+    void *params[] = {(void *)&status};
+    const hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.probe, 1, 1, 1, 64, 1, 1, 0, nullptr, params, nullptr);
+    return e == hipSuccess ? 0 : -1;
 }
 
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
