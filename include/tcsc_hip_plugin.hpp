@@ -26,6 +26,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "ternary_spgemm.h"
@@ -54,8 +55,9 @@ public:
         init(matrix, rows, cols);
     }
     // From any TCSC-shaped object with the reference's public vectors
-    // (class TCSC, data_structures/TCSC.h:5-11).
-    template <class TCSCLike>
+    // (class TCSC, data_structures/TCSC.h:5-11).  Class types only: a raw
+    // `int *` (main.cpp's W_raw.data()) is the dense-matrix ctor above.
+    template <class TCSCLike, class = std::enable_if_t<std::is_class<TCSCLike>::value>>
     HipTCSC(const TCSCLike &t, int K, int N, int device = -1) : K_(K), N_(N), device_(device)
     {
         tsg_tcsc *h = nullptr;

@@ -1,0 +1,126 @@
+// plugin_ref_check.cpp -- the drop-in (include/tcsc_hip_plugin.hpp) compiled
+// against the reference's OWN headers, read in place from /root/reference
+// (never copied): cpp_impl/common.h (comp_func, comp_func_prelu, add_function,
+// TCSC, BlockedTCSC, ...), data_structures/DataStructureInterface.hpp and
+// sparseUtils.h (initX, generateSparseMatrix, GEMM, GEMM_PreLU,
+// compare_results).  The plugin is built with TSG_WITH_REFERENCE_DSI, so
+// tsg::HipTCSC really derives from the reference's DataStructureInterface
+// (DataStructureInterface.hpp:4-14) and overrides its two pure virtuals.
+//
+// Registration is written exactly as INTEGRATION.md section 2 shows a
+// maintainer adding it to cpp_impl/main.cpp:63-81, and the correctness loop
+// is the reference's own (main.cpp:192-247): fresh Y, call, compare_results
+// against the dense GEMM, "Test case <name> passed!" or exit(1).
+//
+// TEST INFRASTRUCTURE: built by `make -C oracle refplugin` into
+// oracle/_ref/plugin_ref_check (gitignored; travels to the GPU box like
+// libref.so).  tests/test_integration_ref.py builds it on the CPU (compile +
+// link = the ABI and the interface match); tests/test_gpu_parity.py runs it
+// on the GPU when present.  Without a device it only reports that it linked.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "data_structures/DataStructureInterface.hpp"
+#include "sparseUtils.h"
+#define TSG_WITH_REFERENCE_DSI
+#include "tcsc_hip_plugin.hpp"
+
+// the registry of main.cpp:12-33 (its definitions live in main.cpp, which has
+// its own main(); the declarations come from common.h:15-16)
+static std::vector<comp_func> userFuncs;
+static std::vector<std::string> funcNames;
+static std::vector<comp_func_prelu> userFuncs_prelu;
+static std::vector<std::string> funcNames_prelu;
+
+void add_function(comp_func f, std::string name)
+{
+    userFuncs.push_back(f);
+    funcNames.push_back(name);
+}
+
+void add_prelu_function(comp_func_prelu f, std::string name)
+{
+    userFuncs_prelu.push_back(f);
+    funcNames_prelu.push_back(name);
+}
+
+int main(int argc, char **argv)
+{
+    // positional argv as main.cpp:49-52: -M m -K k -N n -s s
+    int M = 96, K = 1536, N = 700, s = 4;
+    if (argc >= 9) {
+        M = std::atoi(argv[2]);
+        K = std::atoi(argv[4]);
+        N = std::atoi(argv[6]);
+        s = std::atoi(argv[8]);
+    }
+    int ndev = 0;
+    if (tcsc_hip_device_count(&ndev) != TSG_OK || ndev == 0) {
+        std::printf("plugin_ref_check: built and linked against the reference headers; no HIP device, not run\n");
+        return 0;
+    }
+
+    std::vector<int> W_raw = generateSparseMatrix<int>(K, N, s, false);  // main.cpp:60
+
+    // the lines a maintainer adds to main.cpp
+    auto sf_csc = std::make_shared<TCSC>(W_raw.data(), K, N);                            // main.cpp:63
+    add_function(tsg::make_hip_comp_func(*sf_csc, K, N), "HipBaseTCSC");
+    auto sf_blocked = std::make_shared<BlockedTCSC<512>>(W_raw.data(), K, N);            // main.cpp:69
+    add_function(tsg::make_hip_comp_func(*sf_blocked, K, N), "HipBaseBlockedTCSC");
+    auto hip = std::make_shared<tsg::HipTCSC>(*sf_csc, K, N);
+    add_prelu_function(tsg::make_hip_comp_func_prelu(hip), "HipBaseTCSC_PreLU");
+
+    // DataStructureInterface (DataStructureInterface.hpp:10-13) through the base class
+    std::unique_ptr<DataStructureInterface> dsi(new tsg::HipTCSC(W_raw.data(), K, N));
+    const std::vector<int> back = dsi->getVectorRepresentation(K, N);
+    if (back != W_raw) {
+        std::printf("DataStructureInterface round trip failed\n");
+        return 1;
+    }
+    std::printf("DataStructureInterface round trip passed!\n");
+
+    // main.cpp:192-247
+    std::vector<float> X_main = initX<float>(M * K, 512);
+    std::vector<float> W_FP32_main(W_raw.begin(), W_raw.end());
+    std::vector<float> B_main(N, 2);
+    std::vector<float> alpha_main(N, 0.1);
+    std::vector<float> Y_main(M * N, 0);
+    std::vector<float> refY_main(M * N, 0);
+    std::vector<float> refY_prelu_main(M * N, 0);
+    GEMM(X_main.data(), W_FP32_main.data(), B_main.data(), refY_main.data(), M, N, K);
+    GEMM_PreLU(X_main.data(), W_FP32_main.data(), B_main.data(), alpha_main.data(), refY_prelu_main.data(), M, N, K);
+    // BlockedTCSC<512> drops rows past (K/512)*512 (BlockedTCSC.h:17): its reference is
+    // the GEMM of that truncated W
+    std::vector<float> W_blk(W_FP32_main);
+    for (size_t i = (size_t)(K / 512) * 512 * N; i < W_blk.size(); i++) W_blk[i] = 0;
+    std::vector<float> refY_blk(M * N, 0);
+    GEMM(X_main.data(), W_blk.data(), B_main.data(), refY_blk.data(), M, N, K);
+
+    for (size_t i = 0; i < userFuncs.size(); i++) {
+        std::fill(Y_main.begin(), Y_main.end(), 0);
+        userFuncs[i](X_main.data(), B_main.data(), Y_main.data(), M, N, K);
+        const std::vector<float> &ref = funcNames[i] == "HipBaseBlockedTCSC" ? refY_blk : refY_main;
+        if (compare_results(Y_main.data(), const_cast<float *>(ref.data()), M, N)) {
+            std::printf("Test case %s passed!\n", funcNames[i].c_str());
+        } else {
+            std::printf("Test case %s failed!\n", funcNames[i].c_str());
+            return 1;
+        }
+    }
+    for (size_t i = 0; i < userFuncs_prelu.size(); i++) {
+        std::fill(Y_main.begin(), Y_main.end(), 0);
+        userFuncs_prelu[i](X_main.data(), B_main.data(), alpha_main.data(), Y_main.data(), M, N, K);
+        if (compare_results(Y_main.data(), refY_prelu_main.data(), M, N)) {
+            std::printf("Test case %s passed!\n", funcNames_prelu[i].c_str());
+        } else {
+            std::printf("Test case %s failed!\n", funcNames_prelu[i].c_str());
+            return 1;
+        }
+    }
+    return 0;
+}

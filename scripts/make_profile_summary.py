@@ -33,19 +33,22 @@ if trace:
             w.writeheader()
             w.writerows(rows)
 
-tot = collections.defaultdict(lambda: collections.defaultdict(float))
-disp = collections.defaultdict(lambda: collections.defaultdict(set))
+# per (pass, kernel, counter): total and dispatches; a counter collected in
+# several passes (GRBM_GUI_ACTIVE) is averaged over them, not summed
+tot = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
+disp = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(set)))
 for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "tsg" not in k:
+        if "tsg" not in k or "probe" in k:
             continue
         kn = k.split("(")[0].replace("void ", "").strip()
-        tot[kn][r["Counter_Name"]] += float(r["Counter_Value"])
-        disp[kn][r["Counter_Name"]].add(r["Dispatch_Id"])
+        tot[kn][r["Counter_Name"]][f] += float(r["Counter_Value"])
+        disp[kn][r["Counter_Name"]][f].add(r["Dispatch_Id"])
 out = {"workload": f"{M}x{K}x{N}s{s}", "kernel": None, "kernels": {}, "per_launch_hbm_bytes": {}}
 for kn, v in tot.items():
-    per = {c: x / max(len(disp[kn][c]), 1) for c, x in v.items()}
+    per = {c: sum(x / max(len(disp[kn][c][f]), 1) for f, x in passes.items()) / len(passes)
+           for c, passes in v.items()}
     o = {"per_launch": per}
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
         o["hbm_read_bytes"] = 2 * per["FETCH_SIZE"] * 1024  # guide's gfx950 correction (see the calibration below)
@@ -63,8 +66,14 @@ for kn, v in tot.items():
         if "FETCH_SIZE" in per and per["FETCH_SIZE"]:
             o["read_bytes_over_fetch_size_bytes"] = o["hbm_read_bytes_by_request_size"] / (per["FETCH_SIZE"] * 1024)
     if "SQC_ICACHE_BUSY_CYCLES" in per and "GRBM_GUI_ACTIVE" in per:
-        # SQC counters are summed over the SQCs (one per CU pair: 128); GRBM over 8 XCDs
+        # summed over the instruction caches (one SQC per CU pair: 128 on the chip);
+        # GRBM_GUI_ACTIVE over the 8 XCDs
         o["sqc_icache_busy_frac"] = per["SQC_ICACHE_BUSY_CYCLES"] / 128 / (per["GRBM_GUI_ACTIVE"] / 8)
+    if "SQ_ACTIVE_INST_VALU" in per and "GRBM_GUI_ACTIVE" in per:
+        # a wave64 VALU instruction occupies its SIMD 4 cycles (1024 SIMDs)
+        o["valu_busy_frac"] = 4 * per["SQ_ACTIVE_INST_VALU"] / 1024 / (per["GRBM_GUI_ACTIVE"] / 8)
+    if "SQ_WAIT_INST_ANY" in per and "SQ_WAVE_CYCLES" in per:
+        o["wave_time_waiting_for_instructions"] = per["SQ_WAIT_INST_ANY"] / per["SQ_WAVE_CYCLES"]
     if "SQC_ICACHE_HITS" in per and "SQC_ICACHE_REQ" in per and per["SQC_ICACHE_REQ"]:
         o["sqc_icache_hit_rate"] = per["SQC_ICACHE_HITS"] / per["SQC_ICACHE_REQ"]
     if "SQ_LDS_IDX_ACTIVE" in per and "GRBM_GUI_ACTIVE" in per:

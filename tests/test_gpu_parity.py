@@ -358,3 +358,22 @@ def test_blocked_tcsc_errors(tsg, oracle_mod, monkeypatch):
     monkeypatch.setenv("TSG_KERNEL", "rx")
     with pytest.raises(tsg.TSGError, match="jit kernel only"):
         tsg.TCSCDevice.from_blocked(*blk, 64, 8, 16)
+
+
+def test_plugin_against_reference_headers():
+    """oracle/_ref/plugin_ref_check (built in the build container from the
+    reference's own common.h / DataStructureInterface.hpp / sparseUtils.h,
+    tests/test_integration_ref.py): the reference's generateSparseMatrix, TCSC
+    and BlockedTCSC<512> ctors, dense GEMM / GEMM_PreLU and compare_results
+    around the registered HIP comp_funcs, as main.cpp:192-247 runs them."""
+    import subprocess
+    from conftest import REPO
+    exe = os.path.join(REPO, "oracle", "_ref", "plugin_ref_check")
+    if not os.path.exists(exe):
+        pytest.skip("plugin_ref_check not built (needs the reference headers in the build container)")
+    for argv in ([], ["-M", "130", "-K", "1100", "-N", "300", "-s", "2"]):
+        r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        for name in ("HipBaseTCSC", "HipBaseBlockedTCSC", "HipBaseTCSC_PreLU"):
+            assert f"Test case {name} passed!" in r.stdout, r.stdout
+        assert "DataStructureInterface round trip passed!" in r.stdout
