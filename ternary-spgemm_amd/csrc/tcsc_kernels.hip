@@ -69,6 +69,54 @@ __global__ __launch_bounds__(256) void tsg_transpose4_kernel(const float *__rest
     }
 }
 
+// X [M][K] -> the k-pair layout of the jit kernel (tsg_internal.h): for k-row
+// pair p and M-row pair mp the 16 bytes at (p * Mp/2 + mp) * 16 hold
+// X[2mp][2p], X[2mp+1][2p], X[2mp][2p+1], X[2mp+1][2p+1]; zero outside M x K.
+// A 64 (m) x 64 (k) tile goes through LDS: loads along k (16 B per lane when
+// VEC: K % 4 == 0 and X 16-byte aligned), stores 16 B per lane, consecutive
+// lanes on consecutive mp (coalesced 512-B runs per pair row).  HBM-bound:
+// 8 * M * K bytes.
+template <bool VEC>
+__global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *__restrict__ X,
+                                                                  float *__restrict__ XP, int M, int K,
+                                                                  int Mp, int Kp)
+{
+    __shared__ float tile[64][65];  // [m][k]
+    const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+    if (VEC) {
+        const int c4 = (threadIdx.x & 15) * 4, r = threadIdx.x >> 4;  // 16 x 16
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int ml = r + 16 * i, m = m0 + ml, k = k0 + c4;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (m < M && k < K) v = *reinterpret_cast<const float4 *>(X + (size_t)m * K + k);  // K % 4 == 0
+            tile[ml][c4] = v.x;
+            tile[ml][c4 + 1] = v.y;
+            tile[ml][c4 + 2] = v.z;
+            tile[ml][c4 + 3] = v.w;
+        }
+    } else {
+        const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int m = m0 + ty + 4 * i, k = k0 + tx;
+            tile[ty + 4 * i][tx] = (m < M && k < K) ? X[(size_t)m * K + k] : 0.0f;
+        }
+    }
+    __syncthreads();
+    // 32 pairs x 32 M pairs of float4 per tile: 4 per thread
+    const int mpl = threadIdx.x & 31, pl0 = threadIdx.x >> 5;  // 32 x 8
+    const size_t half_mp = (size_t)Mp / 2;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int pl = pl0 + 8 * i, p = (k0 >> 1) + pl;
+        if (2 * p >= Kp) continue;
+        const int a = 2 * mpl, kk = 2 * pl;
+        *reinterpret_cast<float4 *>(XP + ((size_t)p * half_mp + (size_t)(m0 >> 1) + mpl) * 4) =
+            make_float4(tile[a][kk], tile[a + 1][kk], tile[a][kk + 1], tile[a + 1][kk + 1]);
+    }
+}
+
 // One LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS
 // [lds_dst, lds_dst + 1 KiB).  Inline asm on purpose: hipcc cannot prove that
 // later ds_reads do not alias an in-flight LDS-DMA and would put
@@ -222,6 +270,20 @@ int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, vo
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+
+int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int Kp, void *stream)
+{
+    // Mp is a multiple of 128 (the jit M tile) and Kp of 96: the 64 x 64 tiles
+    // cover [0, Kp) x [0, Mp) exactly in m and up to 32 pad rows in k
+    dim3 grid((unsigned)((Kp + 63) / 64), (unsigned)(Mp / 64));
+    if (K % 4 == 0 && ((uintptr_t)X & 15) == 0)
+        hipLaunchKernelGGL(tsg_transpose_pairs_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, X, XP, M, K,
+                           Mp, Kp);
+    else
+        hipLaunchKernelGGL(tsg_transpose_pairs_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, X, XP, M, K,
+                           Mp, Kp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                    const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,

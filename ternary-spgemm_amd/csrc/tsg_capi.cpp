@@ -318,7 +318,8 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     if (K == 0) {
         // no X at all: chain is +0; X^T stays zero
         HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
-    } else if (tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s) != 0) {
+    } else if ((h->kind == tsg_tcsc::kJit ? tsg::launch_transpose_pairs(dX, h->d_work, M, K, Mp, Kp, s)
+                                          : tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s)) != 0) {
         return fail(TSG_ERR_HIP, std::string("transpose launch: ") + hipGetErrorString(hipGetLastError()));
     }
     int slot = -1;
@@ -439,7 +440,7 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     if (B < 0) return fail(TSG_ERR_ARG, "negative block size");
     std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, B);
     if (!e.empty()) return fail(TSG_ERR_ARG, std::string(B ? "malformed BlockedTCSC: " : "malformed TCSC: ") + e);
-    if (B && tsg::kJitSlots - tsg::kJitNW / 2 < 4)
+    if (B && (tsg::kJitXRegs - tsg::kJitNW) / tsg::kJitSlotRegs < 2)
         return fail(TSG_ERR_ARG, "BlockedTCSC: this jit kernel geometry has no registers for the block sums");
     const int64_t slots = (B ? (int64_t)(K / B) : 1) * N;
     int ndev = 0;

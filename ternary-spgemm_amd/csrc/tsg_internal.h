@@ -64,43 +64,39 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 // ---------------------------------------------------------------------------
 // "jit" (weight-compiled) kernel: dispatcher tsg_jit_kernel (tsg_jit_kernel.hip,
 // built as the code object lib/tsg_jit.co) + machine code generated from the
-// TCSC arrays (tsg_jit.cpp).  A workgroup covers kJitTileM M rows (2 per lane)
-// x kJitTileCols columns; each generated stream owns kJitNW columns and is run
-// by kJitMSplit waves (one per 128-row M slice); X^T chunks of kJitChunk K rows
-// in a ring of kJitRing LDS buffers (3 x 48 KiB; ring 2: 2 x 64 KiB).  Geometry (compile time, TSG_JIT_GEOM,
-// shared with tsg_jit_kernel.hip):
-//   1 (default): 8 waves x 64 columns x 128 M rows, 48 X slots, 2 waves/SIMD
-//   2:          16 waves x 32 columns x 128 M rows, 24 X slots, 4 waves/SIMD
-//   3:           8 waves = 4 streams x 2 M slices, 64 columns, 256 M rows:
-//                pairs of waves share a stream (instruction fetch)
-#ifndef TSG_JIT_GEOM
-#define TSG_JIT_GEOM 1
-#endif
-constexpr int kJitTileM = TSG_JIT_GEOM == 3 ? 256 : 128;
-constexpr int kJitWaves = TSG_JIT_GEOM == 2 ? 16 : 8;
-constexpr int kJitMSplit = TSG_JIT_GEOM == 3 ? 2 : 1;
+// TCSC arrays (tsg_jit.cpp).  A workgroup covers kJitTileM = 128 M rows (2 per
+// lane) x kJitTileCols columns: 8 waves, each running the generated stream of
+// kJitNW columns; X^T chunks of kJitChunk K rows in a ring of kJitRing LDS
+// buffers (3 x 48 KiB), staged by LDS-DMA two steps ahead.
+//
+// X^T layout ("k-pair" layout, written by tsg_transpose_pairs_kernel): rows
+// come in pairs p = (2p, 2p+1), and for M row pair mp = (2mp, 2mp+1) the 16
+// bytes at ((p * Mp/2) + mp) * 16 hold
+//     X[2mp][2p], X[2mp+1][2p], X[2mp][2p+1], X[2mp+1][2p+1]
+// so one ds_read_b128 of lane l (M rows m0 + 2l, m0 + 2l + 1) loads BOTH k
+// rows of a pair into a 4-VGPR X slot: row 2p in v[s:s+1], row 2p+1 in
+// v[s+2:s+3] (a pair with one used row is read with ds_read_b64 into v[s:s+1]).
+// An M tile's slice of a pair row is 64 lanes x 16 B = 1 KiB: one LDS-DMA piece.
+constexpr int kJitTileM = 128;
+constexpr int kJitWaves = 8;
+constexpr int kJitMSplit = 1;
 constexpr int kJitStreams = kJitWaves / kJitMSplit;     // streams per column tile
-constexpr int kJitNW = TSG_JIT_GEOM == 2 ? 32 : 64;
+constexpr int kJitNW = 64;
 constexpr int kJitTileCols = kJitStreams * kJitNW;
-// TSG_JIT_RING: LDS buffers in the X^T ring.  3 (default): 96-row chunks, each
-// staged two steps ahead; 2 (geometry 1 only): 128-row chunks (2 x 64 KiB),
-// staged one step ahead -- a third fewer steps (barriers), no read-ahead
-// across a barrier.
-#ifndef TSG_JIT_RING
-#define TSG_JIT_RING 3
-#endif
-constexpr int kJitRing = TSG_JIT_RING;
-static_assert(kJitRing == 3 || (kJitRing == 2 && TSG_JIT_GEOM == 1), "2-buffer ring: geometry 1 only");
-constexpr int kJitChunk = TSG_JIT_GEOM == 3 ? 48 : kJitRing == 2 ? 128 : 96;
-constexpr int kJitSlots = TSG_JIT_GEOM == 2 ? 24 : 48;  // X slot registers v[8 : 8 + 2 * slots)
+constexpr int kJitRing = 3;
+constexpr int kJitChunk = 96;                           // K rows per chunk (48 pairs)
+constexpr int kJitXRegs = 96;                           // X slot registers v[8 : 8 + 96)
+constexpr int kJitSlotRegs = 4;                         // one X slot = one k-row pair (2 x 2 M rows)
+constexpr int kJitSlots = kJitXRegs / kJitSlotRegs;     // 24 X slots
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
+constexpr uint32_t kJitFormat = 2;                      // region header word 7 bits 8+: k-pair layout
 
 // Stream width: columns per generated stream.  kJitNW (64) is the default;
 // narrower streams (32, 16, 8: same register contract, fewer accumulators,
 // dispatcher lib/tsg_jit_w<nw>.co) give small-M calls more workgroups
 // (tsg_capi.cpp pick_jit_width).  BlockedTCSC runs at kJitNW only.
 constexpr int kJitWidths[] = {kJitNW, 32, 16, 8};
-inline bool jit_width_ok(int nw) { return nw == kJitNW || (TSG_JIT_GEOM == 1 && (nw == 32 || nw == 16 || nw == 8)); }
+inline bool jit_width_ok(int nw) { return nw == kJitNW || nw == 32 || nw == 16 || nw == 8; }
 
 struct JitImage {
     int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0;
@@ -138,6 +134,8 @@ int encode_fill(const int32_t *dW, int K, int N, const int32_t *d_csp, const int
 
 // Kernel launchers (csrc/tcsc_kernels.hip).  All enqueue on `stream`.
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream);
+// X [M][K] -> X^T in the k-pair layout of the jit kernel (Kp even, Mp even)
+int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int Kp, void *stream);
 int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                    const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                    int prelu, void *stream);

@@ -67,6 +67,13 @@ struct Emit {
         c.push_back(0xd8ec0000u | off);
         c.push_back((d << 24) | a);
     }
+    // ds_read_b128 v[d:d+3], v[a] offset:off   (a k-row pair: both rows of the lane's 2 M rows)
+    void ds_read_b128(uint32_t d, uint32_t a, uint32_t off)
+    {
+        align8();
+        c.push_back(0xd9fe0000u | off);
+        c.push_back((d << 24) | a);
+    }
     // global_load_lds_dwordx4 v[voff], s[84:85]   (LDS-DMA, destination M0)
     void glds_x4(uint32_t voff)
     {
@@ -106,30 +113,36 @@ struct Emit {
     uint32_t pos_bytes() const { return (uint32_t)(c.size() * 4); }
 };
 
-// Register contract (tsg_jit_kernel.hip): X slots v[8 : 8 + 2S), then kJitRing LDS
-// buffer bases, the code-prefetch sink, the DMA piece offsets, lane*128, and
-// the accumulators from the next even register.
-constexpr uint32_t kRowBytes = kJitTileM * 4;             // one X^T row of the tile in LDS
-constexpr uint32_t kBufBytes = kJitChunk * kRowBytes;     // one LDS chunk buffer
-constexpr int kPieceRows = 1024 / kRowBytes;              // rows per 1-KiB LDS-DMA piece
-constexpr int kPieces = kJitChunk / kPieceRows / kJitWaves;  // DMA pieces per wave per chunk
-static_assert(kPieces * kPieceRows * kJitWaves == kJitChunk, "chunk rows split in pieces over the waves");
-constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 2s : 9 + 2s]
-constexpr uint32_t kLdsBaseV = kXSlot0 + 2 * kJitSlots;   // + b: lane row 0 of LDS buffer b
+// Register contract (tsg_jit_kernel.hip): X slots v[8 : 8 + 96) (24 slots of 4
+// VGPRs: one k-row pair each), then kJitRing LDS buffer bases (buffer + lane *
+// 16), the code-prefetch sink, the DMA piece offsets, lane*128, and the
+// accumulators from the next even register.
+constexpr uint32_t kPairBytes = kJitTileM * 8;            // one k-row pair of the tile in LDS: 1 KiB
+constexpr uint32_t kBufBytes = kJitChunk / 2 * kPairBytes; // one LDS chunk buffer (48 KiB)
+constexpr int kPieces = kJitChunk / 2 / kJitWaves;        // DMA pieces (pair rows) per wave per chunk
+static_assert(kPieces * kJitWaves * 2 == kJitChunk, "chunk pairs split in pieces over the waves");
+static_assert(kPairBytes == 1024, "one LDS-DMA piece (64 lanes x 16 B) is one pair row");
+constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 4s : 11 + 4s]
+constexpr uint32_t kLdsBaseV = kXSlot0 + kJitXRegs;        // + b: buffer b + lane * 16
 constexpr uint32_t kSinkV = kLdsBaseV + kJitRing;
 constexpr uint32_t kDmaOffV = kSinkV + 1;                  // + i: DMA piece i offsets
 constexpr uint32_t kLane128V = kDmaOffV + kPieces;
 constexpr uint32_t kAcc0 = (kLane128V + 2) & ~1u;         // column c: v[acc0 + 2c : acc0 + 2c + 1]
-static_assert(kAcc0 + 2 * kJitNW <= (TSG_JIT_GEOM == 2 ? 128u : 256u), "VGPR budget");
+static_assert(kAcc0 + 2 * kJitNW <= 256u, "VGPR budget");
 // narrower streams (jit width < kJitNW) use the same register contract, fewer accumulators
 constexpr int kTailPad = 32768 + 1024;   // words of padding after the last stream (code prefetch reads ahead)
-static_assert((kJitChunk - 1) * kRowBytes < 65536, "ds_read offset field");
+static_assert((kJitChunk / 2 - 1) * kPairBytes + 8 < 65536, "ds_read offset field");
 
-// One step's work for a wave: the chunk rows its columns use, ascending, and
-// per row the columns with an entry there (pos or neg pass of the step).
+// One step's work for a wave: its X reads (k-row pairs of the chunk with an
+// entry in the step, ascending) and, per read, the columns with an entry in
+// the even / odd row of the pair.
 struct Section {
-    std::vector<int> rows;
-    std::vector<std::vector<uint8_t>> cols;
+    struct Read {
+        int pair = 0;
+        int mask = 0;                      // 1: even row used, 2: odd row, 3: both
+        std::vector<uint8_t> cols[2];
+    };
+    std::vector<Read> reads;
 };
 
 // One step of a stream: the X^T chunk staged into LDS buffer q % kJitRing and which
@@ -188,32 +201,32 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     const int nch = img.nch, ntiles = img.Npad / tile_cols;
     const std::vector<StepSpec> plan = plan_steps(K, N, B, nch, nw);
     const int steps = (int)plan.size();
-    // X slots: all of v[8 : lds) for BaseTCSC; BlockedTCSC keeps y of half the
+    // X slots: all of v[8 : 104) for BaseTCSC; BlockedTCSC keeps y of half the
     // columns (nw registers) at the top of that range
-    const int S = B ? kJitSlots - nw / 2 : kJitSlots;
-    const uint32_t kTmp0 = kXSlot0 + 2u * (uint32_t)S;  // y of column c0 + c: v[tmp0 + 2c : +1]
+    const int S = B ? (kJitXRegs - nw) / kJitSlotRegs : kJitSlots;
+    const uint32_t kTmp0 = kXSlot0 + (uint32_t)(kJitSlotRegs * S);  // y of column c0 + c: v[tmp0 + 2c : +1]
     img.wcode.assign((size_t)ntiles * kJitStreams, 0u);
     std::vector<uint32_t> &code = img.code;
     code.clear();
     const int64_t slots = (B ? (int64_t)(K / B) : 1) * N;
     const int64_t nnz = (int64_t)csp[slots] + (int64_t)csn[slots];
-    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitStreams * ((size_t)steps * 220 + 64) + kTailPad + 64);
+    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitStreams * ((size_t)steps * 150 + 64) + kTailPad + 64);
     // header: magic, then the geometry (tests/test_jit_codegen.py derives the
-    // register contract from it), the block size and the X slots in use
+    // register contract from it), the block size, the X slots in use, the
+    // ring and the X^T layout
     code.insert(code.end(), {kJitMagic0, kJitMagic1,
                              (uint32_t)kJitWaves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
                              (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
-                             (uint32_t)kJitRing});
+                             (uint32_t)kJitRing | kJitFormat << 8});
     Emit E{code};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
-    // prefetch), nolgkm (no LDS waits), noreads (no X reads), halfreads (every
-    // other X read: the instruction count of 2-row reads)
+    // prefetch), nolgkm (no LDS waits), noreads (no X reads)
     const std::string diag = std::getenv("TSG_JIT_DIAG") ? std::getenv("TSG_JIT_DIAG") : "";
     auto has = [&](const char *f) { return diag.find(f) != std::string::npos; };
     const bool d_nobar = has("nobar"), d_nodma = has("nodma"), d_notouch = has("notouch"),
-               d_nolgkm = has("nolgkm"), d_noreads = has("noreads"), d_halfreads = has("halfreads");
+               d_nolgkm = has("nolgkm"), d_noreads = has("noreads");
     // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,1)
     uint32_t touch_first = 1, touch_count = 1;
     if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
@@ -225,7 +238,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     int n0 = 0;  // first column of the current stream
     std::vector<int32_t> cur((size_t)nw * 2), end((size_t)nw * 2);
     std::vector<uint8_t> live(nw, 0);  // BlockedTCSC: y of the column holds an entry
-    // step q's section: consumes the wave's entries in rows [klo, khi) of its pass
+    // step q's section: the wave's entries in rows [klo, khi) of its pass, as
+    // X reads: one per k-row pair with an entry (ascending), its used rows and
+    // per row the columns with an entry there
     auto build_section = [&](int q, Section &sec) {
         const StepSpec &sp = plan[(size_t)q];
         const int p = sp.pass, kc = sp.chunk * kJitChunk;
@@ -242,13 +257,17 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             const int32_t e = end[(size_t)col * 2 + p];
             for (; i < e && ri[i] < sp.khi; i++) by_row[ri[i] - kc].push_back((uint8_t)col);
         }
-        sec.rows.clear();
-        sec.cols.clear();
-        for (int r = 0; r < kJitChunk; r++)
-            if (!by_row[r].empty()) {
-                sec.rows.push_back(r);
-                sec.cols.push_back(std::move(by_row[r]));
-            }
+        sec.reads.clear();
+        for (int pr = 0; pr < kJitChunk / 2; pr++) {
+            const bool lo = !by_row[2 * pr].empty(), hi = !by_row[2 * pr + 1].empty();
+            if (!lo && !hi) continue;
+            Section::Read rd;
+            rd.pair = pr;
+            rd.mask = (lo ? 1 : 0) | (hi ? 2 : 0);
+            if (lo) rd.cols[0] = std::move(by_row[2 * pr]);
+            if (hi) rd.cols[1] = std::move(by_row[2 * pr + 1]);
+            sec.reads.push_back(std::move(rd));
+        }
     };
     int base_chunk = -1;  // chunk whose base s[84:85] holds
     // stage step q's chunk into LDS buffer q % kJitRing; M0 = s83 (this wave's first
@@ -265,32 +284,32 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         base_chunk = j;
         E.nop(4);  // SALU-written SGPR base -> VMEM
         for (int i = 0; i < kPieces; i++) {
-            E.m0_wave((uint32_t)(q % kJitRing) * kBufBytes + (uint32_t)i * 1024u);
+            E.m0_wave((uint32_t)(q % kJitRing) * kBufBytes + (uint32_t)i * kPairBytes);
             E.nop(0);  // M0 -> LDS-DMA
             E.glds_x4(kDmaOffV + (uint32_t)i);
         }
     };
 
-    // X row schedule.  The wave's used rows, over all steps, form one sequence
-    // g = 0, 1, ...; row g lives in X slot g % S.  Rows are processed
-    // in groups of G (never across a step): at a group's start the wave waits
-    // (counted lgkmcnt; LDS returns in order) for the group's reads, then
-    // issues the reads of the following rows up to RA rows past the group (at
-    // most into the next step, whose chunk is already resident), then adds the
-    // group's entries -- column by column (pairs interleaved) or row by row.
-    // Every column meets its rows in ascending k either way.
-    // TSG_JIT_READS="G,RA,order" (order 0 = column-major, 1 = row-major);
-    // default S/2,S/2,0 (the block schedule: one group of reads in flight).
-    // Reads run ahead into the next step only when its chunk is already
-    // resident (ring 3: staged two steps ahead, visible since the last barrier);
-    // with 2 buffers the next chunk lands at this step's closing barrier.
-    const int kLook = kJitRing == 3 ? 1 : 0;
-    int G = S / 2, RA = S / 2, row_major = 0;
-    if (const char *rv = std::getenv("TSG_JIT_READS")) std::sscanf(rv, "%d,%d,%d", &G, &RA, &row_major);
+    // X read schedule.  The wave's reads (k-row pairs with an entry), over all
+    // steps, form one sequence g = 0, 1, ...; read g lives in X slot g % S.
+    // Reads are consumed in groups of G (never across a step): at a group's
+    // start the wave waits (counted lgkmcnt; LDS returns in order) for the
+    // group's reads, then issues the reads of the following pairs up to RA
+    // past the group (at most into the next step, whose chunk is already
+    // resident: staged two steps ahead, visible since the last barrier), then
+    // adds the group's entries column by column (pairs of columns
+    // interleaved).  Every column meets its rows in ascending k.
+    // TSG_JIT_READS="G,RA" overrides the default S/2,S/2.
+    int G = S / 2, RA = S / 2;
+    if (const char *rv = std::getenv("TSG_JIT_READS")) std::sscanf(rv, "%d,%d", &G, &RA);
     if (G < 1 || RA < 0 || G + RA > S) {
         G = S / 2;
         RA = S / 2;
     }
+    // register of row `half` (0: even k, 1: odd k) of read g
+    auto xreg = [&](int64_t g, const Section::Read &rd, int half) {
+        return kXSlot0 + (uint32_t)(kJitSlotRegs * (g % S)) + (rd.mask == 3 ? 2u * (uint32_t)half : 0u);
+    };
     for (int t = 0; t < ntiles; t++) {
         for (int w = 0; w < kJitStreams; w++) {
             while (code.size() % 64) E.nop();  // 256-B aligned stream start
@@ -306,30 +325,32 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 E.barrier();
             }
             std::vector<Section> secs(steps);
-            std::vector<int64_t> first(steps + 1, 0);  // global index of each step's first row
+            std::vector<int64_t> first(steps + 1, 0);  // global index of each step's first read
             int built = 0;
             auto ensure = [&](int q) {
                 while (built <= q && built < steps) {
                     build_section(built, secs[built]);
-                    first[built + 1] = first[built] + (int64_t)secs[built].rows.size();
+                    first[built + 1] = first[built] + (int64_t)secs[built].reads.size();
                     built++;
                 }
             };
             int64_t issued = 0, ready = 0;  // reads issued / reads known complete
-            int rq = 0;                      // step of row `issued`
-            // issue reads up to row `upto` (exclusive), not past step `qmax`
+            int rq = 0;                      // step of read `issued`
+            // issue reads up to `upto` (exclusive), not past step `qmax`
             auto issue_reads = [&](int64_t upto, int qmax) {
                 qmax = std::min(qmax, steps - 1);
                 for (; issued < upto; issued++) {
                     while (rq + 1 <= qmax && issued >= first[rq + 1]) rq++;
                     if (issued >= first[rq + 1]) return;  // past step qmax
-                    const int r = secs[rq].rows[(size_t)(issued - first[rq])];
-                    if (!d_noreads && !(d_halfreads && (issued & 1)))
-                        E.ds_read_b64(kXSlot0 + 2u * (uint32_t)(issued % S), kLdsBaseV + (uint32_t)(rq % kJitRing),
-                                      (uint32_t)r * kRowBytes);
+                    const Section::Read &rd = secs[rq].reads[(size_t)(issued - first[rq])];
+                    if (d_noreads) continue;
+                    const uint32_t dst = kXSlot0 + (uint32_t)(kJitSlotRegs * (issued % S));
+                    const uint32_t lb = kLdsBaseV + (uint32_t)(rq % kJitRing), off = (uint32_t)rd.pair * kPairBytes;
+                    if (rd.mask == 3) E.ds_read_b128(dst, lb, off);
+                    else E.ds_read_b64(dst, lb, off + (rd.mask == 2 ? 8u : 0u));
                 }
             };
-            auto wait_rows = [&](int64_t upto) {  // rows < upto complete
+            auto wait_reads = [&](int64_t upto) {  // reads < upto complete
                 if (ready >= upto) return;
                 const int64_t n = std::min<int64_t>(std::max<int64_t>(issued - upto, 0), 15);
                 if (!d_nolgkm) E.wait_lgkm((uint32_t)n);
@@ -364,31 +385,25 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     E.code_touch(kSinkV, kLane128V);
                 }
                 const Section &sec = secs[q];
-                const int nrow = (int)sec.rows.size();
-                for (int i0 = 0; i0 < nrow; i0 += G) {
-                    const int i1 = std::min(nrow, i0 + G);
+                const int nrd = (int)sec.reads.size();
+                for (int i0 = 0; i0 < nrd; i0 += G) {
+                    const int i1 = std::min(nrd, i0 + G);
                     const int64_t g1 = first[q] + i1;
                     issue_reads(g1, q);  // (only if the schedule left the group unread)
-                    wait_rows(g1);
-                    issue_reads(g1 + RA, q + kLook);
-                    if (row_major) {
-                        for (int i = i0; i < i1; i++) {
-                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % S);
-                            for (uint8_t col : sec.cols[i]) add(col, x);
-                        }
-                    } else {
-                        // per column its entries of the group; columns in pairs, interleaved
-                        std::vector<std::vector<uint32_t>> xs(nw);
-                        for (int i = i0; i < i1; i++) {
-                            const uint32_t x = kXSlot0 + 2u * (uint32_t)((first[q] + i) % S);
-                            for (uint8_t col : sec.cols[i]) xs[col].push_back(x);
-                        }
-                        for (int col = sp.c0; col < sp.c1; col += 2)
-                            for (size_t k = 0; k < std::max(xs[col].size(), xs[col + 1].size()); k++) {
-                                if (k < xs[col].size()) add(col, xs[col][k]);
-                                if (k < xs[col + 1].size()) add(col + 1, xs[col + 1][k]);
-                            }
+                    wait_reads(g1);
+                    issue_reads(g1 + RA, q + 1);
+                    // per column its entries of the group (ascending k); columns in pairs, interleaved
+                    std::vector<std::vector<uint32_t>> xs(nw);
+                    for (int i = i0; i < i1; i++) {
+                        const Section::Read &rd = sec.reads[(size_t)i];
+                        for (int half = 0; half < 2; half++)
+                            for (uint8_t col : rd.cols[half]) xs[col].push_back(xreg(first[q] + i, rd, half));
                     }
+                    for (int col = sp.c0; col < sp.c1; col += 2)
+                        for (size_t k = 0; k < std::max(xs[col].size(), xs[col + 1].size()); k++) {
+                            if (k < xs[col].size()) add(col, xs[col][k]);
+                            if (k < xs[col + 1].size()) add(col + 1, xs[col + 1][k]);
+                        }
                 }
                 if (sp.flush)  // comp.h:642: Y += y (a block without entries adds +0: a no-op, Y is never -0)
                     for (int col = sp.c0; col < sp.c1; col++)
@@ -396,7 +411,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                             E.pk_acc(kAcc0 + 2u * (uint32_t)col, kTmp0 + 2u * (uint32_t)(col - sp.c0));
                             live[col] = 0;
                         }
-                issue_reads(first[q + 1] + std::max(G, RA), q + kLook);  // next step's first rows (ring 3)
+                issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
                 E.wait_vm(ntouch);
                 if (!d_nobar) E.barrier();
             }
@@ -549,7 +564,7 @@ extern "C" int tsg_jit_codegen_w(const int32_t *csp, const int32_t *csn, const i
         g_tsg_host_err = std::string(B ? "tsg_jit_codegen: malformed BlockedTCSC: " : "tsg_jit_codegen: malformed TCSC: ") + e;
         return TSG_ERR_ARG;
     }
-    if (B && tsg::kJitSlots - tsg::kJitNW / 2 < 4) {
+    if (B && (tsg::kJitXRegs - tsg::kJitNW) / tsg::kJitSlotRegs < 2) {
         g_tsg_host_err = "tsg_jit_codegen: this kernel geometry has no registers for BlockedTCSC";
         return TSG_ERR_ARG;
     }

@@ -6,41 +6,33 @@
 // result with hipModuleLoadData, so the loader maps that code executable
 // together with this kernel.
 //
-// Why compile W into code (DESIGN.md 5): the BaseTCSC chain (comp.h:37-63)
+// Why compile W into code (DESIGN.md 4): the BaseTCSC chain (comp.h:37-63)
 // is one dependent fp32 add per nonzero, and a walk that READS the entry
 // indices at run time pays, per nonzero, for the index (LDS gather or
 // register-indexed add) and per column for a data-dependent branch -- the
 // measured cost of the register-X walk was 2-3x its adds.  Here every nonzero
-// of a wave's 32 columns is one v_pk_add_f32 (2 M rows per lane) whose X
-// register (a row of the current X^T block, loaded by ds_read_b64) and
-// accumulator are encoded in the instruction: no index traffic, no SALU, no
-// branch.  The same code serves every 128-row M tile.
+// of a wave's columns is one v_pk_add_f32 (2 M rows per lane) whose X
+// register (a row of the current X^T chunk, loaded from LDS) and accumulator
+// are encoded in the instruction: no index traffic, no SALU, no branch.  The
+// same code serves every 128-row M tile.
 //
-// Workgroup: kJTileM M rows x kJTileCols columns, one per CU; a wave owns 2
-// rows per lane of one 128-row M slice and the kJNW columns of its stream.
-// Geometry TSG_JIT_GEOM (as tsg_internal.h): 1 (default) 8 waves x 64
-// columns, 2 waves per SIMD, 256 VGPRs; 2: 16 waves x 32 columns, 4 waves per
-// SIMD, 128 VGPRs; 3: 8 waves = 4 streams x 2 M slices (a stream's code is
-// fetched once for 2 waves), 64 columns, 256 M rows.  The dispatcher sets up
-// registers and calls the
-// wave's generated stream ONCE; the stream itself runs the whole K loop:
-// X^T chunks of 96 rows in a ring of 3 LDS buffers, each staged by LDS-DMA two
-// steps ahead, one `s_waitcnt vmcnt(0); s_barrier` per step (step q = pass
-// p * nch + chunk j: p = 0 the +1 entries, p = 1 the -1 entries), the next
-// step's first X rows read before the barrier, the stream's own code touched
-// ahead (L2 prefetch).  TSG_JIT_RING=2: 128-row chunks in 2 buffers, staged one
-// step ahead, no read across a barrier.
-// Register contract (tsg_jit.cpp), S X slots, R ring buffers, P DMA pieces:
-//   v[8 : 8+2S)   X slots (2 M rows each)
-//   next R        LDS byte address of lane row 0 in buffer 0..R-1
-//   next 1        code-prefetch sink
-//   next P        per-lane byte offsets (from the chunk base) of this wave's
-//                 LDS-DMA pieces (2 rows each)
-//   next 1        lane * 128 (code prefetch)
-//   from the next even register: accumulators, column c at acc0 + 2c
-//   GEOM 1: S=48 -> v104-106, v107, v108-113, v114, acc v[116:243]
-//   GEOM 1, ring 2: v104-105, v106, v107-114, v115, acc v[116:243]
-//   GEOM 2: S=24 -> v56-58,   v59,  v60-62,   v63,  acc v[64:127]
+// Workgroup: 128 M rows x (8 waves x kJNW columns), one per CU; a wave owns 2
+// M rows per lane and the kJNW columns of its stream (2 waves per SIMD, 244
+// VGPRs).  The dispatcher sets up registers and calls the wave's generated
+// stream ONCE; the stream runs the whole K loop: X^T chunks of 96 K rows (48
+// k-row pairs, tsg_internal.h "k-pair layout") in a ring of 3 LDS buffers,
+// each staged by LDS-DMA two steps ahead (6 pair rows of 1 KiB per wave), one
+// `s_waitcnt vmcnt(0); s_barrier` per step (step q = pass p * nch + chunk j:
+// p = 0 the +1 entries, p = 1 the -1 entries), X pairs read with ds_read_b128
+// (both k rows at once), the next step's first reads issued before the
+// barrier, the stream's own code touched ahead (L2 prefetch).
+// Register contract (tsg_jit.cpp):
+//   v[8:104)   24 X slots of 4 VGPRs (k-row pair: row 2p in v[s:s+1], 2p+1 in v[s+2:s+3])
+//   v104-106   LDS byte address of lane*16 in ring buffer 0..2
+//   v107       code-prefetch sink
+//   v108-113   per-lane byte offsets (from the chunk base) of this wave's 6 LDS-DMA pieces
+//   v114       lane * 128 (code prefetch)
+//   v[116:244) accumulators, column c at v116 + 2c (rows 2l, 2l+1 of the lane)
 //   s[80:81] X^T base, s82 chunk stride in bytes, s83 LDS byte offset of this
 //   wave's first DMA piece, s[84:85] chunk base (stream),
 //   s86 saved M0, s[88:89] prefetch address (stream), s[92:93] region base,
@@ -51,52 +43,29 @@
 
 namespace {
 
-#ifndef TSG_JIT_GEOM
-#define TSG_JIT_GEOM 1
-#endif
-constexpr int kJWaves = TSG_JIT_GEOM == 2 ? 16 : 8;
-constexpr int kJMSplit = TSG_JIT_GEOM == 3 ? 2 : 1;
-constexpr int kJStreams = kJWaves / kJMSplit;
-// TSG_JIT_NW: a narrower stream width on geometry 1 (32, 16 or 8 columns per
-// wave; lib/tsg_jit_w<NW>.co) -- more workgroups for small M, same registers
+constexpr int kJWaves = 8;
+// TSG_JIT_NW: a narrower stream width (32, 16 or 8 columns per wave;
+// lib/tsg_jit_w<NW>.co) -- more workgroups for small M, same registers
 #ifndef TSG_JIT_NW
-#define TSG_JIT_NW (TSG_JIT_GEOM == 2 ? 32 : 64)
+#define TSG_JIT_NW 64
 #endif
 constexpr int kJNW = TSG_JIT_NW;
-static_assert(TSG_JIT_GEOM == 1 || kJNW == (TSG_JIT_GEOM == 2 ? 32 : 64), "narrow widths: geometry 1 only");
 static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8, "stream width");
-constexpr int kJTileM = TSG_JIT_GEOM == 3 ? 256 : 128;
-constexpr int kJTileCols = kJStreams * kJNW;
-#ifndef TSG_JIT_RING
-#define TSG_JIT_RING 3
-#endif
-constexpr int kJRing = TSG_JIT_RING;  // LDS buffers in the X^T ring (tsg_internal.h)
-static_assert(kJRing == 3 || (kJRing == 2 && TSG_JIT_GEOM == 1), "2-buffer ring: geometry 1 only");
-constexpr int kJChunk = TSG_JIT_GEOM == 3 ? 48 : kJRing == 2 ? 128 : 96;
-constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB (ring 2: 64 KiB)
-constexpr int kJPieceRows = 1024 / (kJTileM * 4);    // X^T rows per 1-KiB LDS-DMA piece
-constexpr int kJPieces = kJChunk / kJPieceRows / kJWaves;  // LDS-DMA pieces per wave per chunk
+constexpr int kJTileM = 128;
+constexpr int kJTileCols = kJWaves * kJNW;
+constexpr int kJRing = 3;                            // LDS buffers in the X^T ring (tsg_internal.h)
+constexpr int kJChunk = 96;                          // K rows per chunk = 48 k-row pairs
+constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB
+constexpr int kJPieces = kJChunk / 2 / kJWaves;      // LDS-DMA pieces (1-KiB pair rows) per wave per chunk
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 typedef float F32x16 __attribute__((ext_vector_type(16)));
 
-// geometry 1/3 register bindings of the LDS bases, DMA piece offsets, lane*128
-// and the code-prefetch sink (tsg_jit.cpp kLdsBaseV...kLane128V)
-#if TSG_JIT_RING == 2
-#define TSG_JIT_IN                                                                                  \
-    "{v104}"(lb0), "{v105}"(lb1), "{v107}"(off[0]), "{v108}"(off[1]), "{v109}"(off[2]),          \
-        "{v110}"(off[3]), "{v111}"(off[4]), "{v112}"(off[5]), "{v113}"(off[6]), "{v114}"(off[7]), \
-        "{v115}"(l128)
-#define TSG_JIT_SINK "v106"
-#else
 #define TSG_JIT_IN                                                                                  \
     "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),             \
         "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
-#define TSG_JIT_SINK "v107"
-#endif
 
-#if TSG_JIT_GEOM != 2
 #define TSG_JIT_CLOBBERS \
     "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", \
         "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", \
@@ -105,16 +74,8 @@ typedef float F32x16 __attribute__((ext_vector_type(16)));
         "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", \
         "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", \
         "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", \
-        "v100", "v101", "v102", "v103", TSG_JIT_SINK, "s84", "s85", "s86", "s88", "s89", "s94", "s95", \
+        "v100", "v101", "v102", "v103", "v107", "s84", "s85", "s86", "s88", "s89", "s94", "s95", \
         "scc", "memory"
-#else
-#define TSG_JIT_CLOBBERS \
-    "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", \
-        "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", \
-        "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", \
-        "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v59", "s84", "s85", "s86", "s88", \
-        "s89", "s94", "s95", "scc", "memory"
-#endif
 
 }  // namespace
 
@@ -192,104 +153,59 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const int loc = wg - cb * kGN * mtiles, g = loc / (wc * kGM), i = loc - g * wc * kGM;
     const int nt = kGN * cb + i % wc, mt = kGM * g + i / wc;
     const int m0 = mt * kJTileM;
-    const int stream = wave % kJStreams, ms = wave / kJStreams;  // column stream, 128-row M slice
+    const int stream = wave;  // the wave's column stream
     const int ncol0 = nt * kJTileCols + stream * kJNW;
-
-#ifdef TSG_JIT_SAMETILE  // diagnostic (results WRONG): every workgroup runs column tile 0's code
-    const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[stream]);
-#else
-    const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJStreams + stream]);
-#endif
-    const uint32_t lb0 = (uint32_t)(ms * 512 + lane * 8), lb1 = lb0 + kJBufBytes;
-    [[maybe_unused]] const uint32_t lb2 = lb0 + 2 * kJBufBytes;  // ring 3 only
-    // LDS-DMA piece i of this wave: chunk rows kJPieceRows*(wave*P + i) + lane / (64 / kJPieceRows)
-    constexpr int kLanesPerRow = 64 / kJPieceRows;
+    const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + stream]);
+    const uint32_t lb0 = (uint32_t)lane * 16u, lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
+    // LDS-DMA piece i of this wave = pair row pr = wave * P + i of the chunk: the
+    // lane's 16 B at ((pr * Mp/2) + m0/2 + lane) * 16 from the chunk base
     uint32_t off[kJPieces];
 #pragma unroll
     for (int i = 0; i < kJPieces; i++) {
-        const uint32_t r = (uint32_t)(kJPieceRows * (wave * kJPieces + i) + lane / kLanesPerRow);
-        off[i] = (r * (uint32_t)Mp + (uint32_t)m0 + 4u * (uint32_t)(lane % kLanesPerRow)) * 4u;
+        const uint32_t pr = (uint32_t)(wave * kJPieces + i);
+        off[i] = (pr * ((uint32_t)Mp / 2u) + (uint32_t)m0 / 2u + (uint32_t)lane) * 16u;
     }
     const uint32_t wb = (uint32_t)(wave * kJPieces) * 1024u;  // s83
     const uint32_t l128 = (uint32_t)lane * 128u;
     const uint32_t stride = (uint32_t)kJChunk * (uint32_t)Mp * 4u;
 
-#if TSG_JIT_GEOM != 2 && TSG_JIT_NW == 64
+#define TSG_JIT_CALL(...)                                                                           \
+    asm volatile("s_getpc_b64 s[94:95]\n"                                                           \
+                 ".Ljr%=:\n\t"                                                                      \
+                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"                                        \
+                 "s_addc_u32 s95, s95, 0\n\t"                                                       \
+                 "s_setpc_b64 %[cp]\n"                                                              \
+                 ".Ljb%=:"                                                                          \
+                 : __VA_ARGS__                                                                      \
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb), \
+                   TSG_JIT_IN                                                                       \
+                 : TSG_JIT_CLOBBERS)
+#if TSG_JIT_NW == 64
     F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
-    asm volatile("s_getpc_b64 s[94:95]\n"
-                 ".Ljr%=:\n\t"
-                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
-                 "s_addc_u32 s95, s95, 0\n\t"
-                 "s_setpc_b64 %[cp]\n"
-                 ".Ljb%=:"
-                 : "+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3)
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   TSG_JIT_IN
-                 : TSG_JIT_CLOBBERS);
+    TSG_JIT_CALL("+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3));
     auto acc_of = [&](int c, int r) {
         return c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
              : c < 48 ? a2[2 * (c & 15) + r] : a3[2 * (c & 15) + r];
     };
-#elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 32
+#elif TSG_JIT_NW == 32
     F32x32 a0 = {}, a1 = {};  // comp.h:41
-    asm volatile("s_getpc_b64 s[94:95]\n"
-                 ".Ljr%=:\n\t"
-                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
-                 "s_addc_u32 s95, s95, 0\n\t"
-                 "s_setpc_b64 %[cp]\n"
-                 ".Ljb%=:"
-                 : "+{v[116:147]}"(a0), "+{v[148:179]}"(a1)
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   TSG_JIT_IN
-                 : TSG_JIT_CLOBBERS);
+    TSG_JIT_CALL("+{v[116:147]}"(a0), "+{v[148:179]}"(a1));
     auto acc_of = [&](int c, int r) { return c < 16 ? a0[2 * (c & 15) + r] : a1[2 * (c & 15) + r]; };
-#elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 16
+#elif TSG_JIT_NW == 16
     F32x32 a0 = {};  // comp.h:41
-    asm volatile("s_getpc_b64 s[94:95]\n"
-                 ".Ljr%=:\n\t"
-                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
-                 "s_addc_u32 s95, s95, 0\n\t"
-                 "s_setpc_b64 %[cp]\n"
-                 ".Ljb%=:"
-                 : "+{v[116:147]}"(a0)
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   TSG_JIT_IN
-                 : TSG_JIT_CLOBBERS);
-    auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
-#elif TSG_JIT_GEOM == 1 && TSG_JIT_NW == 8
-    F32x16 a0 = {};  // comp.h:41
-    asm volatile("s_getpc_b64 s[94:95]\n"
-                 ".Ljr%=:\n\t"
-                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
-                 "s_addc_u32 s95, s95, 0\n\t"
-                 "s_setpc_b64 %[cp]\n"
-                 ".Ljb%=:"
-                 : "+{v[116:131]}"(a0)
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   TSG_JIT_IN
-                 : TSG_JIT_CLOBBERS);
+    TSG_JIT_CALL("+{v[116:147]}"(a0));
     auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
 #else
-    F32x32 a0 = {}, a1 = {};  // comp.h:41
-    asm volatile("s_getpc_b64 s[94:95]\n"
-                 ".Ljr%=:\n\t"
-                 "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"
-                 "s_addc_u32 s95, s95, 0\n\t"
-                 "s_setpc_b64 %[cp]\n"
-                 ".Ljb%=:"
-                 : "+{v[64:95]}"(a0), "+{v[96:127]}"(a1)
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb),
-                   "{v56}"(lb0),
-                   "{v57}"(lb1), "{v58}"(lb2), "{v60}"(off[0]), "{v61}"(off[1]), "{v62}"(off[2]),
-                   "{v63}"(l128)
-                 : TSG_JIT_CLOBBERS);
-    auto acc_of = [&](int c, int r) { return c < 16 ? a0[2 * (c & 15) + r] : a1[2 * (c & 15) + r]; };
+    F32x16 a0 = {};  // comp.h:41
+    TSG_JIT_CALL("+{v[116:131]}"(a0));
+    auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
 #endif
+#undef TSG_JIT_CALL
 
     if (ncol0 >= N) return;
 #pragma unroll
     for (int r = 0; r < 2; r++) {
-        const int m = m0 + ms * 128 + 2 * lane + r;
+        const int m = m0 + 2 * lane + r;
         if (m >= M) continue;
         float *yrow = Y + (size_t)m * N + ncol0;
         float v[kJNW];

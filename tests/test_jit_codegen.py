@@ -2,9 +2,11 @@
 runs it.  tsg_jit_codegen's region is decoded instruction by instruction (only
 the gfx950 encodings the generator may emit are accepted) and a whole
 workgroup is emulated against the register contract of
-ternary-spgemm_amd/csrc/tsg_jit_kernel.hip: its 16 waves run barrier phase by
-barrier phase, LDS-DMA copies land at the issuing wave's `s_waitcnt vmcnt(n)` (VMEM loads
-return in order: all but the newest n),
+ternary-spgemm_amd/csrc/tsg_jit_kernel.hip and the k-pair X^T layout of
+tsg_internal.h: its 8 waves run barrier phase by barrier phase, LDS-DMA
+copies (one 1-KiB k-row pair per piece) land at the issuing wave's
+`s_waitcnt vmcnt(n)` (VMEM loads return in order: all but the newest n),
+ds_read_b128 loads both rows of a pair (ds_read_b64 one of them),
 and every LDS read is checked to see data that landed in an EARLIER phase (no
 read-after-DMA race) while no DMA may overwrite rows read since it was issued
 (no write-after-read race).  Code-prefetch loads must stay inside the region.
@@ -21,7 +23,7 @@ MAGIC = (0x7453474A, 0x314A4954)
 
 
 class Geom:
-    """Geometry from the region header (words 2-3) and the register contract
+    """Geometry from the region header (words 2-7) and the register contract
     of tsg_jit_kernel.hip derived from it."""
 
     def __init__(self, code):
@@ -29,22 +31,23 @@ class Geom:
         self.waves, self.nw, self.chunk = w2 & 0xFF, (w2 >> 8) & 0xFF, w2 >> 16
         self.slots, self.tile_m = w3 & 0xFFFF, w3 >> 16
         self.streams, self.msplit = w4 & 0xFF, (w4 >> 8) & 0xFF
-        assert self.streams * self.msplit == self.waves and self.tile_m == 128 * self.msplit
+        assert self.streams == self.waves and self.msplit == 1 and self.tile_m == 128
         self.tile_cols = self.streams * self.nw
-        self.row_bytes = self.tile_m * 4
-        self.buf_bytes = self.chunk * self.row_bytes
-        self.piece_rows = 1024 // self.row_bytes
-        self.pieces = self.chunk // self.piece_rows // self.waves
-        self.ring = int(code[7]) or 3  # LDS buffers in the X^T ring (TSG_JIT_RING)
-        self.lds_v = 8 + 2 * self.slots
+        self.ring = int(code[7]) & 0xFF
+        assert int(code[7]) >> 8 == 2, "region must use the k-pair X^T layout (format 2)"
+        self.pairs = self.chunk // 2                  # k-row pairs per chunk
+        self.pair_bytes = self.tile_m * 8             # one pair row of the tile in LDS: 1 KiB
+        self.buf_bytes = self.pairs * self.pair_bytes
+        self.pieces = self.pairs // self.waves        # DMA pieces (pair rows) per wave
+        self.lds_v = 8 + 4 * self.slots               # X slots: 4 VGPRs each
         self.sink_v = self.lds_v + self.ring
         self.dma_v = self.sink_v + 1
         self.l128_v = self.dma_v + self.pieces
         self.acc0 = (self.l128_v + 2) & ~1
-        # BlockedTCSC<B> (B > 0): X slots v[8 : 8 + 2 xslots), block sums y above them
+        # BlockedTCSC<B> (B > 0): X slots v[8 : 8 + 4 xslots), block sums y above them
         self.B = int(code[5])
         self.xslots = int(code[6]) or self.slots
-        self.tmp0 = 8 + 2 * self.xslots
+        self.tmp0 = 8 + 4 * self.xslots
 
 
 XT_BASE = 1 << 40  # fake device address of X^T
@@ -62,7 +65,7 @@ class Wave:
         self.touch = None
         self.pending = []  # VMEM loads not yet returned, oldest first: the DMA copies of one
         #                    global_load_lds [(lds_byte, data, issue_phase)...] or [] (code touch)
-        self.reads = []    # X slot registers of LDS reads not yet waited for, oldest first
+        self.reads = []    # (first VGPR, count) of LDS reads not yet waited for, oldest first
         self.done = False
 
 
@@ -76,7 +79,7 @@ def _classify_pk(w0, w1, G):
     assert (w1 >> 29) & 1 == neg0 and (w1 >> 30) & 1 == neg1, "neg_lo and neg_hi disagree"
     assert (w1 >> 18) & 0x1FF == 0 and (w1 >> 27) & 3 == 3 and (w0 >> 11) & 0x1F == 8  # op_sel_hi, clamp/opsel
     s0, s1 = w1 & 0x1FF, (w1 >> 9) & 0x1FF
-    x_lo, x_hi = 8, 8 + 2 * G.xslots
+    x_lo, x_hi = 8, 8 + 4 * G.xslots
     acc = G.acc0 <= d < G.acc0 + 2 * G.nw
     tmp = G.B and G.tmp0 <= d < G.tmp0 + G.nw
     assert d % 2 == 0
@@ -120,28 +123,34 @@ def _decode(code, pc, G):
         return kind, f, 2
     if (w0 & 0xFFFF0000) == 0xD8EC0000:  # ds_read_b64
         assert (w1 >> 8) & 0xFFFF == 0
-        return "read", (w1 >> 24, w1 & 0xFF, w0 & 0xFFFF), 2
+        return "read", (w1 >> 24, w1 & 0xFF, w0 & 0xFFFF, 2), 2
+    if (w0 & 0xFFFF0000) == 0xD9FE0000:  # ds_read_b128
+        assert (w1 >> 8) & 0xFFFF == 0
+        return "read", (w1 >> 24, w1 & 0xFF, w0 & 0xFFFF, 4), 2
     raise AssertionError(f"unexpected instruction word {w0:#010x} at word {pc}")
 
 
-def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
-    """One workgroup (column tile t, M tile at m0): returns acc[tile rows, tile cols]."""
+def _overlaps(reads, r0, n):
+    return any(a < r0 + n and r0 < a + m for a, m in reads)
+
+
+def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
+    """One workgroup (column tile t, M tile at m0) over the k-pair X^T XP
+    [pairs][Mp/2][4]: returns acc[tile rows, tile cols]."""
     G = Geom(code)
-    WAVES, NW, CHUNK, TILE_M, ROW_BYTES, BUF_BYTES, PIECES = (G.waves, G.nw, G.chunk, G.tile_m, G.row_bytes,
-                                                            G.buf_bytes, G.pieces)
+    WAVES, NW, PAIRS, PAIR_BYTES, BUF_BYTES, PIECES = (G.waves, G.nw, G.pairs, G.pair_bytes, G.buf_bytes,
+                                                       G.pieces)
     region_bytes = len(code) * 4
-    stride = CHUNK * Mp * 4
-    lanes = np.arange(64)
+    stride = G.chunk * Mp * 4
     NBUF = G.ring
     lds = np.zeros(NBUF * BUF_BYTES // 4, np.float32)
-    landed = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)   # phase a row's data landed
-    last_read = np.full(NBUF * BUF_BYTES // ROW_BYTES, -1)
+    landed = np.full(NBUF * PAIRS, -1)   # phase a pair row's data landed
+    last_read = np.full(NBUF * PAIRS, -1)
     S = G.streams
-    waves = [Wave(w, int(wcode[t * S + w % S]) // 4) for w in range(WAVES)]
+    waves = [Wave(w, int(wcode[t * S + w]) // 4) for w in range(WAVES)]
     for wv in waves:
         wv.v[G.acc0:G.acc0 + 2 * NW] = 0.0
-    for wv in waves:
-        assert int(wcode[t * S + wv.w % S]) % 256 == 0
+        assert int(wcode[t * S + wv.w]) % 256 == 0
     phase = 0
     while not all(wv.done for wv in waves):
         at_barrier = 0
@@ -176,44 +185,44 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                 elif kind == "glds":
                     i = f[0] - G.dma_v
                     assert 0 <= i < PIECES
-                    chunk_row0 = G.piece_rows * (wv.w * PIECES + i)
+                    pr = wv.w * PIECES + i  # the pair row this lane set copies (dispatcher off[i])
                     j, rem = divmod(wv.base - XT_BASE, stride)
                     assert rem == 0 and 0 <= j < nch
-                    assert wv.m0 % BUF_BYTES == chunk_row0 * ROW_BYTES, "DMA lands on the wrong rows"
-                    wv.pending.append([(wv.m0 + half * ROW_BYTES, XT[j * CHUNK + chunk_row0 + half,
-                                                                       m0:m0 + TILE_M].copy(), phase)
-                                       for half in range(G.piece_rows)])
+                    assert wv.m0 % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
+                    data = XP[j * PAIRS + pr, m0 // 2:m0 // 2 + 64].reshape(-1).copy()
+                    wv.pending.append([(wv.m0, data, phase)])
                 elif kind == "wait_vm":  # loads return in order: all but the newest f[0] land
                     n_land = max(len(wv.pending) - f[0], 0)
                     for op in wv.pending[:n_land]:
                         for dst, data, iss in op:
-                            row = dst // ROW_BYTES
-                            assert last_read[row] < iss, "DMA overwrites a row read since its issue (WAR race)"
-                            lds[dst // 4:dst // 4 + TILE_M] = data
+                            row = dst // PAIR_BYTES
+                            assert last_read[row] < iss, "DMA overwrites a pair row read since its issue (WAR race)"
+                            lds[dst // 4:dst // 4 + 256] = data
                             landed[row] = phase
                     wv.pending = wv.pending[n_land:]
                 elif kind == "wait_lgkm":
                     while len(wv.reads) > f[0]:  # LDS returns in order
                         wv.reads.pop(0)
                 elif kind == "read":
-                    vd, a, off = f
-                    assert vd not in wv.reads, "X slot reloaded before its previous read was waited for"
-                    wv.reads.append(vd)
-                    assert G.lds_v <= a < G.lds_v + NBUF and off % ROW_BYTES == 0 and off // ROW_BYTES < CHUNK
-                    assert 8 <= vd < 8 + 2 * G.xslots
-                    row = (a - G.lds_v) * CHUNK + off // ROW_BYTES
+                    vd, a, off, nreg = f
+                    assert not _overlaps(wv.reads, vd, nreg), "X slot reloaded before its previous read was waited for"
+                    wv.reads.append((vd, nreg))
+                    assert G.lds_v <= a < G.lds_v + NBUF and off // PAIR_BYTES < PAIRS
+                    assert 8 <= vd and vd + nreg <= 8 + 4 * G.xslots and (vd - 8) % 4 == 0
+                    half = (off % PAIR_BYTES) // 8
+                    assert off % 8 == 0 and off % PAIR_BYTES in ((0,) if nreg == 4 else (0, 8))
+                    row = (a - G.lds_v) * PAIRS + off // PAIR_BYTES
                     assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
                     last_read[row] = max(last_read[row], phase)
-                    ms = wv.w // S  # the wave's 128-row M slice of the 256- or 128-row tile
-                    vals = lds[row * TILE_M + ms * 128:row * TILE_M + ms * 128 + 128]
-                    wv.v[vd:vd + 2] = vals.reshape(64, 2).T
+                    vals = lds[row * 256:row * 256 + 256].reshape(64, 4)  # lane l: 16 B at lane*16
+                    wv.v[vd:vd + nreg] = vals[:, 2 * half:2 * half + nreg].T
                 elif kind == "add":
                     d, x, neg = f
-                    assert x not in wv.reads, "add reads an X slot whose LDS read may not have returned"
+                    assert not _overlaps(wv.reads, x, 2), "add reads an X slot whose LDS read may not have returned"
                     wv.v[d:d + 2] = wv.v[d:d + 2] - wv.v[x:x + 2] if neg else wv.v[d:d + 2] + wv.v[x:x + 2]
                 elif kind == "first":
                     d, x, neg = f
-                    assert x not in wv.reads, "add reads an X slot whose LDS read may not have returned"
+                    assert not _overlaps(wv.reads, x, 2), "add reads an X slot whose LDS read may not have returned"
                     xv = -wv.v[x:x + 2] if neg else wv.v[x:x + 2]
                     wv.v[d:d + 2] = xv + np.float32(0.0)
                 elif kind == "flush":
@@ -222,29 +231,37 @@ def emulate_tile(code, wcode, t, XT, m0, Mp, nch):
                     wv.v[t:t + 2] = np.nan  # a block sum is consumed once
         assert at_barrier in (0, WAVES), "waves disagree on the barrier count"
         phase += 1
-    acc = np.zeros((TILE_M, G.tile_cols), np.float32)
+    acc = np.zeros((128, G.tile_cols), np.float32)
     for wv in waves:
-        ms, st = wv.w // S, wv.w % S
         for c in range(NW):
             for r in range(2):
-                acc[ms * 128 + r:ms * 128 + 128:2, st * NW + c] = wv.v[G.acc0 + 2 * c + r]
+                acc[r:128:2, wv.w * NW + c] = wv.v[G.acc0 + 2 * c + r]
     return acc
+
+
+def to_pairs(XT):
+    """X^T [Kp][Mp] (Kp, Mp even) -> the k-pair layout [Kp/2][Mp/2][4]
+    (tsg_internal.h; tsg_transpose_pairs_kernel)."""
+    Kp, Mp = XT.shape
+    q = XT.reshape(Kp // 2, 2, Mp // 2, 2)           # [p][k&1][mp][m&1]
+    return np.ascontiguousarray(q.transpose(0, 2, 1, 3).reshape(Kp // 2, Mp // 2, 4))
 
 
 def emulate(code, wcode, X, K, N):
     assert tuple(int(x) for x in code[:2]) == MAGIC
     G = Geom(code)
-    TILE_M, CHUNK, WAVES, TILE_COLS = G.tile_m, G.chunk, G.waves, G.tile_cols
+    CHUNK, TILE_COLS = G.chunk, G.tile_cols
     M = X.shape[0]
     nch = max(1, -(-K // CHUNK))
-    Mp = -(-max(M, 1) // TILE_M) * TILE_M
+    Mp = -(-max(M, 1) // 128) * 128
     XT = np.zeros((nch * CHUNK, Mp), np.float32)
     XT[:K, :M] = X.T
+    XP = to_pairs(XT)
     ntiles = len(wcode) // G.streams
     Y = np.zeros((Mp, ntiles * TILE_COLS), np.float32)
     for t in range(ntiles):
-        for m0 in range(0, Mp, TILE_M):
-            Y[m0:m0 + TILE_M, t * TILE_COLS:(t + 1) * TILE_COLS] = emulate_tile(code, wcode, t, XT, m0, Mp, nch)
+        for m0 in range(0, Mp, 128):
+            Y[m0:m0 + 128, t * TILE_COLS:(t + 1) * TILE_COLS] = emulate_tile(code, wcode, t, XP, m0, Mp, nch)
     return Y[:M, :N]
 
 
