@@ -133,6 +133,17 @@ int tcsc_hip_reserve(tsg_tcsc *h, int max_M);
 int tcsc_hip_jit_width(const tsg_tcsc *h, int M);
 int tcsc_hip_set_jit_width(tsg_tcsc *h, int width);
 
+/* Small-M kernel (no reference counterpart; DESIGN.md 4 "Small M"): calls
+ * with few rows (GEMV-like, M <= 32 by default) on a plain-TCSC handle run an
+ * index-reading sliced-ELL walk (tsg_tcsc_ell_kernel) that reads X in place
+ * and streams its entry stream from HBM once per M tile, instead of the
+ * weight-compiled kernel.  Same results bit for bit.  mode: 0 = automatic
+ * (default), 1 = never, 2 = every call (tests).  The image is built on the
+ * first call that needs it (or tcsc_hip_reserve).
+ * tcsc_hip_call_kernel: the kernel a call with M rows launches. */
+int tcsc_hip_set_small_m(tsg_tcsc *h, int mode);
+const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M);
+
 /* ---- introspection ------------------------------------------------------- */
 typedef struct tsg_info {
     int32_t K, N, device, abi_version;
@@ -227,6 +238,15 @@ int tsg_jit_codegen_w(const int32_t *col_start_pos, const int32_t *col_start_neg
 int tsg_blocked_tcsc_validate(const int32_t *col_start_pos, const int32_t *col_start_neg,
                               const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
                               int B);
+
+/* The small-M kernel's sliced-ELL image for an M tile of MT rows and K chunks
+ * of at most Cmax rows (tsg_ell.hip header): entry words (2 uint16 LDS float
+ * indices each) and per (16-column slice, step) {offset in 256-B units,
+ * 8-entry blocks}; *C, *nch: chunk rows and chunks.  Host only; NULL buffers
+ * query the lengths (in uint32). */
+int tsg_ell_build(const int32_t *col_start_pos, const int32_t *col_start_neg, const int32_t *row_index_pos,
+                  const int32_t *row_index_neg, int K, int N, int Cmax, int MT, uint32_t *ent, int64_t ent_cap,
+                  int64_t *ent_len, uint32_t *tab, int64_t tab_cap, int64_t *tab_len, int32_t *C, int32_t *nch);
 
 /* X[i] = integer-valued fp32 U{-range..range} (initX, sparseUtils.h:6-23). */
 int tsg_gen_x(int64_t len, int range, uint64_t seed, float *X);

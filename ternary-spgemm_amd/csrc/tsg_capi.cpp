@@ -51,6 +51,16 @@ struct tsg_tcsc {
     int jit_nch = 0;                      // X^T chunks (all widths)
     int jit_force = 0;                    // tcsc_hip_set_jit_width / TSG_JIT_NW: 0 = auto
     uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
+    // small-M kernel (tsg_ell.hip): one sliced-ELL image per variant, built on
+    // the first call (or tcsc_hip_reserve) that picks the variant
+    struct EllVariant {
+        tsg::EllImage img;                // host metadata (C, nch, ...); arrays freed after upload
+        uint32_t *d_ent = nullptr, *d_tab = nullptr;
+        int64_t bytes = 0;
+        bool ready = false;
+    };
+    EllVariant ell[tsg::kEllVariants];
+    int small_m = 0;                      // tcsc_hip_set_small_m: 0 auto, 1 never, 2 always (plain TCSC only)
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
@@ -76,6 +86,10 @@ struct tsg_tcsc {
 };
 
 namespace {
+
+// Largest M the automatic choice sends to the small-M (ELL) kernel
+// (profiles/r02e_small_m.jsonl: measured crossover against the jit kernel).
+constexpr int kEllAutoMaxM = 32;
 
 struct DeviceGuard {
     int prev = -1;
@@ -274,6 +288,38 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
     return TSG_OK;
 }
 
+// Small-M kernel choice (DESIGN.md 4 "Small M"): the sliced-ELL walk for a
+// plain-TCSC weight-compiled handle when M is small enough that the jit
+// kernel cannot fill the GPU; -1 = the jit (or rx) kernel.  Variant by M tile.
+int pick_ell_variant(const tsg_tcsc *h, int M)
+{
+    if (h->kind != tsg_tcsc::kJit || h->B || h->small_m == 1) return -1;
+    const int v = M <= tsg::kEllTileM[0] ? 0 : M <= tsg::kEllTileM[1] ? 1 : M <= tsg::kEllTileM[2] ? 2 : 3;
+    if (h->small_m == 2) return v;
+    return M <= kEllAutoMaxM ? v : -1;
+}
+
+// Builds and uploads the ELL image of a variant.  Caller holds h->mu.
+int ensure_ell(tsg_tcsc *h, int v)
+{
+    tsg_tcsc::EllVariant &e = h->ell[v];
+    if (e.ready) return TSG_OK;
+    tsg::build_ell_image(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
+                         h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, tsg::kEllMaxC[v], tsg::kEllTileM[v], e.img);
+    DeviceGuard g(h->device);
+    const size_t eb = e.img.ent.size() * 4, tb = std::max<size_t>(e.img.tab.size() * 4, 8);
+    if (hipMalloc(&e.d_ent, eb) != hipSuccess || hipMalloc(&e.d_tab, tb) != hipSuccess)
+        return fail(TSG_ERR_NOMEM, "hipMalloc of the small-M (ELL) image failed");
+    if (hipMemcpy(e.d_ent, e.img.ent.data(), eb, hipMemcpyHostToDevice) != hipSuccess ||
+        (!e.img.tab.empty() && hipMemcpy(e.d_tab, e.img.tab.data(), e.img.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+        return fail(TSG_ERR_HIP, "upload of the small-M (ELL) image failed");
+    e.bytes = (int64_t)(eb + tb);
+    std::vector<uint32_t>().swap(e.img.ent);
+    std::vector<uint32_t>().swap(e.img.tab);
+    e.ready = true;
+    return TSG_OK;
+}
+
 int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, float *dY, int M,
             int N, int K, hipStream_t s, bool prelu)
 {
@@ -293,7 +339,34 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(s, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
-    int rc = ensure_work(h, M, capturing);
+    int rc;
+    const int ev = pick_ell_variant(h, M);
+    if (ev >= 0) {
+        // small M: the ELL walk reads X in place (no X^T staging, no work buffer)
+        if (!h->ell[ev].ready && capturing)
+            return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the small-M kernel, whose image is not "
+                                     "built yet; call tcsc_hip_reserve before capturing");
+        rc = ensure_ell(h, ev);
+        if (rc) return rc;
+        int slot = -1;
+        if (h->timing && !capturing) {
+            rc = harvest_timing(h, false);
+            if (rc) return rc;
+            slot = h->ring_head;
+            HIP_TRY(hipEventRecord(h->ev0[slot], s));
+        }
+        const tsg_tcsc::EllVariant &e = h->ell[ev];
+        if (tsg::launch_tcsc_ell(ev, dX, e.d_ent, e.d_tab, db, dalpha, dY, M, N, K, e.img.C, e.img.nch,
+                                 prelu ? 1 : 0, s) != 0)
+            return fail(TSG_ERR_HIP, std::string("small-M kernel launch: ") + hipGetErrorString(hipGetLastError()));
+        if (slot >= 0) {
+            HIP_TRY(hipEventRecord(h->ev1[slot], s));
+            h->ring_head = (h->ring_head + 1) % tsg_tcsc::kRing;
+            h->ring_count++;
+        }
+        return TSG_OK;
+    }
+    rc = ensure_work(h, M, capturing);
     if (rc) return rc;
     int Mp, Kp;
     dims_for(h, M, Mp, Kp);
@@ -401,6 +474,10 @@ void free_handle(tsg_tcsc *h)
     for (auto &v : h->jv) {
         if (v.d_wcode) (void)hipFree(v.d_wcode);
         v.mod.unload();
+    }
+    for (auto &e : h->ell) {
+        if (e.d_ent) (void)hipFree(e.d_ent);
+        if (e.d_tab) (void)hipFree(e.d_tab);
     }
     if (h->stream) (void)hipStreamDestroy(h->stream);
     for (int i = 0; i < tsg_tcsc::kRing; i++) {
@@ -647,8 +724,18 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
     if (rc || h->kind != tsg_tcsc::kJit) return rc;
     const int mtiles = (std::max(max_M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM;
     for (int mt = 1; mt <= mtiles; mt++) {
-        rc = ensure_jit_variant(h, pick_jit_width(h, std::min(max_M, mt * tsg::kJitTileM)));
+        const int m = std::min(max_M, mt * tsg::kJitTileM);
+        if (pick_ell_variant(h, m) >= 0 && pick_ell_variant(h, std::min(m, (mt - 1) * tsg::kJitTileM + 1)) >= 0)
+            continue;  // every M of this tile runs the small-M kernel
+        rc = ensure_jit_variant(h, pick_jit_width(h, m));
         if (rc) return rc;
+    }
+    for (int v = 0; v < tsg::kEllVariants; v++) {  // the small-M images calls with M <= max_M run
+        const int lo = v == 0 ? 1 : tsg::kEllTileM[v - 1] + 1;
+        if (lo <= std::max(max_M, 1) && pick_ell_variant(h, lo) == v) {
+            rc = ensure_ell(h, v);
+            if (rc) return rc;
+        }
     }
     return TSG_OK;
 }
@@ -668,6 +755,24 @@ extern "C" int tcsc_hip_jit_width(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
     return pick_jit_width(h, M);
+}
+
+extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    if (mode < 0 || mode > 2) return fail(TSG_ERR_ARG, "tcsc_hip_set_small_m: expected 0 (auto), 1 (never) or 2 (always)");
+    if (mode == 2 && (h->kind != tsg_tcsc::kJit || h->B))
+        return fail(TSG_ERR_ARG, "tcsc_hip_set_small_m: the small-M kernel computes plain TCSC (BaseTCSC) only");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->small_m = mode;
+    return TSG_OK;
+}
+
+extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)
+{
+    if (!h) return "";
+    return pick_ell_variant(h, M) >= 0 ? "tsg_tcsc_ell_kernel"
+           : h->kind == tsg_tcsc::kJit ? "tsg_jit_kernel" : "tsg_tcsc_rx_kernel";
 }
 
 extern "C" int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K)
@@ -709,6 +814,7 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     const bool jit = h->kind == tsg_tcsc::kJit;
     int64_t jit_bytes = 0;
     for (const auto &v : h->jv) jit_bytes += v.code_bytes + v.wcode_words * 4;
+    for (const auto &e : h->ell) jit_bytes += e.bytes;
     o->image_bytes = jit ? jit_bytes : (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;
     o->chunk_rows = jit ? tsg::kJitChunk : tsg::kRxChunk;

@@ -80,6 +80,61 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
     img.ent.resize(img.ent.size() + kRxBlockWords, 0u);  // the walk reads one header ahead
 }
 
+// Sliced-ELL entry stream of the small-M kernel (tsg_ell.hip header) for an
+// M tile of MT rows: per 16-column slice and step (pass, K chunk of C rows)
+// every column's entries in ascending k as the uint16 float index
+// (k - chunk base) * MT into the LDS chunk, padded with C * MT (the zero row) to the
+// slice's longest list rounded up to 8; blocks of 256 B = [16 columns][8 entries].
+void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
+                     int Cmax, int MT, EllImage &img)
+{
+    img.C = std::min(Cmax, std::max(4, (K + 3) / 4 * 4));
+    img.nch = std::max(1, (K + img.C - 1) / img.C);
+    img.steps = 2 * img.nch;
+    img.nslices = (N + 15) / 16;
+    const int C = img.C, nch = img.nch, steps = img.steps;
+    img.tab.assign((size_t)img.nslices * steps * 2, 0u);
+    std::vector<uint16_t> e16;
+    e16.reserve((size_t)((int64_t)csp[N] + csn[N]) * 5 / 4 + (size_t)img.nslices * steps * 128);
+    for (int sl = 0; sl < img.nslices; sl++) {
+        int32_t cur[2][16], end[2][16];
+        for (int c = 0; c < 16; c++) {
+            const int n = sl * 16 + c;
+            for (int p = 0; p < 2; p++) {
+                const int32_t *cs = p ? csn : csp;
+                cur[p][c] = n < N ? cs[n] : 0;
+                end[p][c] = n < N ? cs[n + 1] : 0;
+            }
+        }
+        for (int step = 0; step < steps; step++) {
+            const int p = step / nch, j = step % nch;
+            const int32_t *ri = p ? rin : rip;
+            const int khi = (j + 1) * C;
+            int cnt[16], L = 0;
+            for (int c = 0; c < 16; c++) {
+                int q = cur[p][c];
+                while (q < end[p][c] && ri[q] < khi) q++;
+                cnt[c] = q - cur[p][c];
+                L = std::max(L, cnt[c]);
+            }
+            const int n8 = (L + 7) / 8;
+            const size_t at = e16.size();
+            img.tab[((size_t)sl * steps + step) * 2] = (uint32_t)(at / 128);
+            img.tab[((size_t)sl * steps + step) * 2 + 1] = (uint32_t)n8;
+            e16.resize(at + (size_t)n8 * 128, (uint16_t)(C * MT));
+            for (int c = 0; c < 16; c++) {
+                for (int i = 0; i < cnt[c]; i++) {
+                    const int k = ri[cur[p][c] + i];
+                    e16[at + (size_t)(i / 8) * 128 + (size_t)c * 8 + (size_t)(i % 8)] = (uint16_t)((k - j * C) * MT);
+                }
+                cur[p][c] += cnt[c];
+            }
+        }
+    }
+    img.ent.assign((e16.size() + 1) / 2 + 4, 0u);
+    std::memcpy(img.ent.data(), e16.data(), e16.size() * sizeof(uint16_t));
+}
+
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                           const int32_t *rin, int K, int N, int B)
 {
@@ -349,5 +404,32 @@ extern "C" int tsg_csc_packed_to_tcsc(const int32_t *col_ptr, const int32_t *row
     if (csn) csn[N] = (int32_t)q;
     if (nnz_pos) *nnz_pos = p;
     if (nnz_neg) *nnz_neg = q;
+    return TSG_OK;
+}
+
+// Host-only view of the small-M kernel's sliced-ELL image (tests decode it and
+// replay the kernel's walk on the CPU).  NULL buffers query the lengths.
+extern "C" int tsg_ell_build(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K,
+                             int N, int Cmax, int MT, uint32_t *ent, int64_t ent_cap, int64_t *ent_len, uint32_t *tab,
+                             int64_t tab_cap, int64_t *tab_len, int32_t *C, int32_t *nch)
+{
+    const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N);
+    if (!e.empty() || Cmax < 4 || Cmax % 4 || MT < 1 || (int64_t)Cmax * MT >= 65536) {
+        g_tsg_host_err = e.empty() ? "tsg_ell_build: Cmax must be a multiple of 4 with Cmax * MT < 65536"
+                                   : "tsg_ell_build: " + e;
+        return TSG_ERR_ARG;
+    }
+    tsg::EllImage img;
+    tsg::build_ell_image(csp, csn, rip, rin, K, N, Cmax, MT, img);
+    if (ent_len) *ent_len = (int64_t)img.ent.size();
+    if (tab_len) *tab_len = (int64_t)img.tab.size();
+    if (C) *C = img.C;
+    if (nch) *nch = img.nch;
+    if ((ent && ent_cap < (int64_t)img.ent.size()) || (tab && tab_cap < (int64_t)img.tab.size())) {
+        g_tsg_host_err = "tsg_ell_build: buffer too small";
+        return TSG_ERR_ARG;
+    }
+    if (ent) std::memcpy(ent, img.ent.data(), img.ent.size() * 4);
+    if (tab) std::memcpy(tab, img.tab.data(), img.tab.size() * 4);
     return TSG_OK;
 }

@@ -120,6 +120,28 @@ int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t
                     int prelu, uint32_t *status, int tile_cols, void *stream);
 int launch_jit_probe(const JitModule &jm, uint32_t *status);  // legacy default stream
 
+// ---------------------------------------------------------------------------
+// "ell" small-M kernel (tsg_tcsc_ell_kernel, tsg_ell.hip): sliced-ELL entry
+// stream, see the header of tsg_ell.hip.  Variants (template instances):
+//   0:  1 lane per column,  1 M row per lane (M tile 1),  C <= 16380
+//   1:  4 lanes per column, 1 row each       (M tile 4),  C <= 8188
+//   2: 16 lanes per column, 1 row each       (M tile 16), C <= 2044
+//   3: 16 lanes per column, 2 rows each      (M tile 32), C <= 1020
+// (C: K rows per chunk, at most ~128 KiB of LDS per workgroup; entries are
+// float indices r * tile < 65536 into the LDS chunk).
+constexpr int kEllVariants = 4;
+constexpr int kEllTileM[kEllVariants] = {1, 4, 16, 32};
+constexpr int kEllMaxC[kEllVariants] = {16380, 8188, 2044, 1020};
+struct EllImage {
+    int C = 0, nch = 0, steps = 0, nslices = 0;
+    std::vector<uint32_t> ent;   // uint16 entries, 2 per word (256-B blocks)
+    std::vector<uint32_t> tab;   // per (slice, step): {offset in 256-B units, 8-entry blocks}
+};
+void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
+                     int Cmax, int MT, EllImage &img);
+int launch_tcsc_ell(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
+                    const float *alpha, float *Y, int M, int N, int K, int C, int nch, int prelu, void *stream);
+
 // B = 0: plain TCSC; B > 0: BlockedTCSC<B> arrays ((K/B)*N + 1 column starts)
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                           const int32_t *rin, int K, int N, int B = 0);

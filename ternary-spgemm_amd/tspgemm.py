@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "tsg_csc_packed_to_tcsc", "tsg_jit_codegen", "tcsc_hip_kernel_name", "tcsc_hip_encode_dense_dev",
     "tcsc_hip_create_blocked", "tsg_jit_codegen_blocked", "tsg_blocked_tcsc_validate",
     "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tsg_jit_codegen_w",
+    "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build",
 )
 
 
@@ -120,10 +121,15 @@ def lib() -> C.CDLL:
                                           C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tsg_jit_codegen_w.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                     C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
+    L.tcsc_hip_set_small_m.argtypes = [H, C.c_int]
+    L.tcsc_hip_call_kernel.argtypes = [H, C.c_int]
+    L.tcsc_hip_call_kernel.restype = C.c_char_p
+    L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
+                                vp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     L.tcsc_hip_jit_width.argtypes = [H, C.c_int]
     L.tcsc_hip_set_jit_width.argtypes = [H, C.c_int]
     for f in EXPORTED_SYMBOLS:
-        if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name"):
+        if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name", "tcsc_hip_call_kernel"):
             getattr(L, f).restype = C.c_int
     _LIB = L
     return L
@@ -233,6 +239,22 @@ def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0, width: int = 64)
                                nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
            "tsg_jit_codegen")
     return code, wcode
+
+
+def ell_build(csp, csn, rip, rin, K: int, N: int, Cmax: int, MT: int):
+    """Host view of the small-M kernel's sliced-ELL image for an M tile of MT
+    rows (tsg_ell.hip): (entries uint16[] = LDS float indices, tab
+    uint32[slices*steps, 2], C, nch)."""
+    csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
+    ne, nt, c, nch = C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32()
+    L = lib()
+    _check(L.tsg_ell_build(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, Cmax, MT, None, 0, C.byref(ne), None, 0,
+                           C.byref(nt), C.byref(c), C.byref(nch)), "tsg_ell_build")
+    ent = np.empty(ne.value, np.uint32)
+    tab = np.empty(nt.value, np.uint32)
+    _check(L.tsg_ell_build(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, Cmax, MT, _ptr(ent), ne.value,
+                           C.byref(ne), _ptr(tab), nt.value, C.byref(nt), C.byref(c), C.byref(nch)), "tsg_ell_build")
+    return ent.view(np.uint16), tab.reshape(-1, 2), c.value, nch.value
 
 
 def tcsc_to_blocked(csp, csn, rip, rin, K: int, N: int, B: int):
@@ -474,6 +496,14 @@ class TCSCDevice:
     def set_jit_width(self, width: int) -> None:
         """0 = automatic per call (default); 64/32/16/8 pins the stream width."""
         _check(lib().tcsc_hip_set_jit_width(self._h, width), "tcsc_hip_set_jit_width")
+
+    def set_small_m(self, mode: int) -> None:
+        """Small-M kernel: 0 = automatic (default), 1 = never, 2 = every call."""
+        _check(lib().tcsc_hip_set_small_m(self._h, mode), "tcsc_hip_set_small_m")
+
+    def call_kernel(self, M: int) -> str:
+        """Device kernel a call with M rows launches."""
+        return lib().tcsc_hip_call_kernel(self._h, M).decode()
 
     def info(self) -> dict:
         o = tsg_info()

@@ -1,0 +1,61 @@
+"""The small-M kernel's sliced-ELL image (tsg_ell.hip), checked on the CPU
+before any GPU runs it: tsg_ell_build's image is decoded and the kernel's walk
+replayed in numpy -- per 16-column slice and step (pass, K chunk) each
+column's uint16 entries (float indices of X^T rows of an M tile) in order,
+y = y + x in the +1 pass and y = y - x in the -1 pass, padding entries on the
+zero row -- and Y must equal the BaseTCSC oracle (comp.h:25-69) bit for bit,
+for integer and for order-sensitive non-integer X."""
+import numpy as np
+import pytest
+
+
+def replay(ent, tab, C, nch, X, K, N, MT):
+    M = X.shape[0]
+    steps = 2 * nch
+    nslices = (N + 15) // 16
+    tab = tab.reshape(nslices, steps, 2)
+    y = np.zeros((M, nslices * 16), np.float32)
+    for st in range(steps):
+        j = st % nch
+        xs = np.zeros((C + 1, M), np.float32)  # X^T chunk + the zero row
+        rows = min(C, K - j * C)
+        if rows > 0:
+            xs[:rows] = X[:, j * C:j * C + rows].T
+        for sl in range(nslices):
+            off, n8 = (int(v) for v in tab[sl, st])
+            blk = ent[off * 128:(off + n8) * 128].reshape(n8, 16, 8)  # [i8][column][8 entries]
+            for c in range(16):
+                col = sl * 16 + c
+                for u in blk[:, c, :].reshape(-1):
+                    u = int(u)
+                    assert u % MT == 0 and u // MT <= C
+                    x = xs[u // MT]
+                    y[:, col] = y[:, col] - x if st >= nch else y[:, col] + x
+    return y[:, :N]
+
+
+@pytest.mark.parametrize("M,K,N,s,Cmax,MT", [(3, 70, 33, 2, 2048, 4), (5, 300, 40, 4, 256, 32),
+                                             (2, 1100, 17, 8, 512, 16), (4, 9, 5, 1, 4, 4), (1, 1, 1, 1, 16380, 1),
+                                             (1, 5000, 20, 4, 2044, 1), (2, 700, 40, 4, 1020, 32)])
+def test_ell_replay_equals_base_tcsc(tsg, oracle_mod, M, K, N, s, Cmax, MT):
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(K, N, s, M + K + N))
+    ent, tab, C, nch = tsg.ell_build(*t.arrays, K, N, Cmax, MT)
+    assert C <= Cmax and C % 4 == 0 and nch == max(1, -(-K // C))
+    b = np.linspace(-1, 2, N).astype(np.float32)
+    for X in (O.init_x_int(M, K, 3), O.init_x_frac(M, K, 4)):
+        Y = replay(ent, tab, C, nch, X, K, N, MT) + b
+        assert np.array_equal(Y.view(np.uint32), O.base_tcsc(X, t, b).view(np.uint32))
+    # every nonzero appears once; everything else is the zero row, blocks of 8
+    used = ent[:int((tab[:, 0] + tab[:, 1]).max(initial=0)) * 128]  # the blocks (the array has tail padding)
+    real = used[used != C * MT]
+    assert len(real) == len(t.arrays[2]) + len(t.arrays[3])
+
+
+def test_ell_rejects_bad_chunk(tsg, oracle_mod):
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(64, 20, 4, 1))
+    with pytest.raises(tsg.TSGError):
+        tsg.ell_build(*t.arrays, 64, 20, 6, 4)
+    with pytest.raises(tsg.TSGError):
+        tsg.ell_build(*t.arrays, 64, 20, 4096, 16)  # indices past 16 bits

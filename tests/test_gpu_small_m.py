@@ -1,0 +1,133 @@
+"""The small-M kernel (tsg_tcsc_ell_kernel, tsg_ell.hip) on the GPU, through
+the C-ABI: forced onto every call (tcsc_hip_set_small_m(h, 2)) over the edge
+shapes of test_gpu_parity.py, every variant (M tiles of 4, 16 and 32 rows,
+several tiles), PReLU, special values and K chunking; the automatic choice;
+config 3's K and N at M = 1, 16, 64 against the oracle; graph capture after
+reserve.  Bit for bit against the BaseTCSC oracle (comp.h:25-69)."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import EDGE, _bits_eq
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,K,N,s", EDGE)
+def test_edges_forced_small_m(tsg, oracle_mod, M, K, N, s):
+    O = oracle_mod
+    W = O.gen_ternary(K, N, s, M * 7 + K)
+    t = O.tcsc_encode(W)
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.set_small_m(2)
+    assert h.call_kernel(M) == "tsg_tcsc_ell_kernel"
+    b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
+    alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
+    for X in (O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)):
+        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b)), (M, K, N, s)
+        assert _bits_eq(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
+    h.close()
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 16, 17, 31, 32, 33, 64, 100])
+def test_every_variant_and_tiling(tsg, oracle_mod, M):
+    """M picks the variant (tile 4 / 16 / 32); M past a tile runs several tiles.
+    K = 2300 spans several K chunks for every variant (C = 2048 / 512 / 256)."""
+    O = oracle_mod
+    K, N = 2300, 530
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 40 + M))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.set_small_m(2)
+    b = np.linspace(-3, 3, N).astype(np.float32)
+    X = O.init_x_frac(M, K, M)
+    assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b)), M
+    h.close()
+
+
+def test_special_values_small_m(tsg, oracle_mod):
+    from test_gpu_special import _same, _special_b, _special_x
+    O = oracle_mod
+    K, N = 700, 300
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 31))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.set_small_m(2)
+    alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
+    for M, kind in ((3, "mixed"), (9, "subnormal"), (20, "nan"), (7, "zeros")):
+        X = _special_x(M, K, 7, kind)
+        b = _special_b(N, 3)
+        _same(h.gemm(X, b), O.base_tcsc(X, t, b))
+        _same(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
+    h.close()
+
+
+def test_auto_choice_and_structural_edges(tsg, oracle_mod):
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(1024, 4096, 4, 77))
+    h = tsg.TCSCDevice(*t.arrays, 1024, 4096)
+    assert h.call_kernel(1) == "tsg_tcsc_ell_kernel" and h.call_kernel(4096) == "tsg_jit_kernel"
+    h.set_small_m(1)
+    assert h.call_kernel(1) == "tsg_jit_kernel"
+    h.close()
+    # empty / dense / all-zero W and K = 0 on the small-M kernel
+    rng = np.random.default_rng(3)
+    for W in (np.zeros((300, 70), np.int32), rng.integers(-1, 2, size=(260, 150)).astype(np.int32),
+              np.ones((129, 5), np.int32), -np.ones((129, 5), np.int32)):
+        K, N = W.shape
+        W[:, 0] = 0
+        t = O.tcsc_encode(W)
+        h = tsg.TCSCDevice(*t.arrays, K, N)
+        h.set_small_m(2)
+        X = O.init_x_frac(13, K, 9)
+        b = rng.standard_normal(N).astype(np.float32)
+        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+        h.close()
+    h = tsg.TCSCDevice(np.zeros(4, np.int32), np.zeros(4, np.int32), [], [], 0, 3)
+    h.set_small_m(2)
+    Y = h.gemm(np.zeros((5, 0), np.float32), np.array([1.5, -2.0, 0.0], np.float32))
+    assert _bits_eq(Y, np.tile(np.array([1.5, -2.0, 0.0], np.float32), (5, 1)))
+    # BlockedTCSC never takes it
+    blk = O.blocked_tcsc_encode(O.gen_ternary(64, 8, 2, 1), 16)
+    hb = tsg.TCSCDevice.from_blocked(*blk, 64, 8, 16)
+    assert hb.call_kernel(1) == "tsg_jit_kernel"
+    with pytest.raises(tsg.TSGError):
+        hb.set_small_m(2)
+
+
+@pytest.mark.parametrize("M", [1, 16, 32, 64])
+def test_config3_shape_small_m(tsg, oracle_mod, M):
+    """configs[2]'s K = 4096, N = 16384 at GEMV-like M (the reference sweep's
+    M list, plots/run_benchmark.py:8), automatic choice, against the oracle."""
+    import torch
+    O = oracle_mod
+    K, N = 4096, 16384
+    arrs = tsg.gen_tcsc(K, N, 4, 42)
+    h = tsg.TCSCDevice(*arrs, K, N)
+    assert h.call_kernel(M) == ("tsg_tcsc_ell_kernel" if M <= 32 else "tsg_jit_kernel")
+    Xn = O.init_x_frac(M, K, 5)
+    b = np.full(N, 2.0, np.float32)
+    Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+    rows = np.unique(np.r_[0, M // 2, M - 1])
+    ref = O.base_tcsc(np.ascontiguousarray(Xn[rows]), O.TCSC(*arrs, K, N), b)
+    assert _bits_eq(Y[rows], ref)
+    h.close()
+
+
+def test_capture_small_m_after_reserve(tsg, oracle_mod):
+    import torch
+    O = oracle_mod
+    K, N, M = 1024, 2048, 8
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 23))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.reserve(64)
+    assert h.call_kernel(M) == "tsg_tcsc_ell_kernel"
+    b = torch.full((N,), 2.0, device="cuda")
+    Xs = torch.zeros((M, K), device="cuda")
+    Ys = torch.empty((M, N), device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        h.gemm_torch(Xs, b, Ys)
+    Xn = O.init_x_frac(M, K, 1)
+    Xs.copy_(torch.from_numpy(Xn).cuda())
+    g.replay()
+    torch.cuda.synchronize()
+    assert _bits_eq(Ys.cpu().numpy(), O.base_tcsc(Xn, t, np.full(N, 2.0, np.float32)))
+    h.close()
