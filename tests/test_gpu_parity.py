@@ -71,12 +71,16 @@ EDGE = [
 ]
 
 
+@pytest.mark.parametrize("small_m", [0, 1], ids=["auto", "jit-only"])
 @pytest.mark.parametrize("M,K,N,s", EDGE)
-def test_edges_vs_oracle(tsg, oracle_mod, M, K, N, s):
+def test_edges_vs_oracle(tsg, oracle_mod, M, K, N, s, small_m):
+    """Ragged shapes, automatic kernel choice (the small-M kernel for M <= 32)
+    and the weight-compiled kernel forced for every M."""
     O = oracle_mod
     W = O.gen_ternary(K, N, s, M * 7 + K)
     t = O.tcsc_encode(W)
     h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.set_small_m(small_m)
     b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
     alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
     for X in (O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)):
@@ -93,8 +97,9 @@ def test_every_stream_width_vs_oracle(tsg, oracle_mod, width):
         W = O.gen_ternary(K, N, s, M + K + width)
         t = O.tcsc_encode(W)
         h = tsg.TCSCDevice(*t.arrays, K, N)
+        h.set_small_m(1)  # the weight-compiled kernel for every M (M = 1 would take the small-M kernel)
         h.set_jit_width(width)
-        assert h.jit_width(M) == width
+        assert h.jit_width(M) == width and h.call_kernel(M) == "tsg_jit_kernel"
         b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
         alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
         for X in (O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)):
@@ -110,6 +115,7 @@ def test_auto_width_small_m(tsg, oracle_mod):
     K, N = 1024, 4096
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, 77))
     h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.set_small_m(1)
     assert h.jit_width(32) < 64 and h.jit_width(8192) == 64
     b = np.full(N, 2.0, np.float32)
     for M in (32, 8192, 7):
@@ -133,9 +139,10 @@ def test_structural_edges(tsg, oracle_mod):
         W[:, 0] = 0  # an empty column
         t = O.tcsc_encode(W)
         h = tsg.TCSCDevice(*t.arrays, K, N)
-        X = O.init_x_frac(131, K, 9)
         b = rng.standard_normal(N).astype(np.float32)
-        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
+        for M in (131, 7):  # the weight-compiled and the small-M kernel
+            X = O.init_x_frac(M, K, 9)
+            assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b))
     # K = 0: the chain is the +0.0 start, Y = 0 + b
     h = tsg.TCSCDevice(np.zeros(4, np.int32), np.zeros(4, np.int32), [], [], 0, 3)
     Y = h.gemm(np.zeros((5, 0), np.float32), np.array([1.5, -2.0, 0.0], np.float32))
