@@ -32,10 +32,11 @@ namespace {
 // --- gfx950 encodings (checked against llvm-mc -mcpu=gfx950 -show-encoding) ---
 struct Emit {
     std::vector<uint32_t> &c;
+    bool pad8 = std::getenv("TSG_JIT_NOALIGN") == nullptr;  // A/B knob (results unchanged)
     // keep 8-byte instructions 8-byte aligned (hand-asm placement rule)
     void align8()
     {
-        if (c.size() & 1) c.push_back(0xbf800000u);  // s_nop 0
+        if (pad8 && (c.size() & 1)) c.push_back(0xbf800000u);  // s_nop 0
     }
     // v_pk_add_f32 v[d:d+1], v[d:d+1], v[x:x+1] [neg_lo:[0,1] neg_hi:[0,1]]  (VOP3P;
     // the two halves are rows 0 and 1 of the lane: two IEEE adds)
@@ -219,7 +220,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
                              (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
                              (uint32_t)kJitRing | kJitFormat << 8});
-    Emit E{code};
+    Emit E{code, std::getenv("TSG_JIT_NOALIGN") == nullptr};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
     // prefetch), nolgkm (no LDS waits), noreads (no X reads)
@@ -299,12 +300,13 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // resident: staged two steps ahead, visible since the last barrier), then
     // adds the group's entries column by column (pairs of columns
     // interleaved).  Every column meets its rows in ascending k.
-    // TSG_JIT_READS="G,RA" overrides the default S/2,S/2.
-    int G = S / 2, RA = S / 2;
+    // Default G = S/3, RA = 2S/3 (8 and 16 of the 24 slots: measured 0.4% faster
+    // than 12,12, profiles/r02_jit_knobs_ab.txt); TSG_JIT_READS="G,RA" overrides.
+    int G = std::max(1, S / 3), RA = S - std::max(1, S / 3);
     if (const char *rv = std::getenv("TSG_JIT_READS")) std::sscanf(rv, "%d,%d", &G, &RA);
     if (G < 1 || RA < 0 || G + RA > S) {
-        G = S / 2;
-        RA = S / 2;
+        G = std::max(1, S / 3);
+        RA = S - G;
     }
     // register of row `half` (0: even k, 1: odd k) of read g
     auto xreg = [&](int64_t g, const Section::Read &rd, int half) {

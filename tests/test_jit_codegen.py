@@ -323,11 +323,16 @@ def test_jit_code_dense_and_empty_columns(tsg, oracle_mod):
 
 def _count_entry_adds(code, G):
     """v_pk_add_f32 that apply one nonzero (add / first); flushes excluded."""
-    n = 0
-    for i in range(0, len(code) - 1, 2):  # every v_pk_add_f32 is 8-byte aligned
+    n, i = 0, 0
+    while i < len(code) - 1:  # instruction by instruction (8-byte forms aligned or not)
         w0 = int(code[i])
         if (w0 & 0xFFFFFC00) == 0xD3B24000 and (int(code[i + 1]) >> 27) & 3 == 3:
             n += _classify_pk(w0, int(code[i + 1]), G)[0] in ("add", "first")
+            i += 2
+        elif w0 in (0x807CFF53, 0x8058FF5C) or (w0 >> 26) in (0x36, 0x37) or (w0 >> 24) == 0xDD or (w0 >> 24) == 0xDC:
+            i += 2  # literal SALU, DS, global / LDS-DMA: 8 bytes
+        else:
+            i += 1
     return n
 
 
