@@ -134,7 +134,7 @@ int tcsc_hip_jit_width(const tsg_tcsc *h, int M);
 int tcsc_hip_set_jit_width(tsg_tcsc *h, int width);
 
 /* Small-M kernel (no reference counterpart; DESIGN.md 4 "Small M"): calls
- * with few rows (GEMV-like, M <= 32 by default) on a plain-TCSC handle run an
+ * with few rows (GEMV-like, M <= 16 by default) on a plain-TCSC handle run an
  * index-reading sliced-ELL walk (tsg_tcsc_ell_kernel) that reads X in place
  * and streams its entry stream from HBM once per M tile, instead of the
  * weight-compiled kernel.  Same results bit for bit.  mode: 0 = automatic

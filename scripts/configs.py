@@ -55,7 +55,7 @@ def main():
         b = torch.full((N,), 2.0, device=dev)
         Y = torch.empty((M, N), device=dev)
         h.reserve(M)
-        for _ in range(2):
+        for _ in range(20):  # warmup incl. the GPU clock ramp (profiles/r02c_clock_ramp.txt)
             h.gemm_torch(X, b, Y)
         torch.cuda.synchronize()
         h.set_timing(True)
@@ -71,7 +71,7 @@ def main():
         ref = O.base_tcsc(X[:rows].cpu().numpy(), O.TCSC(*arrs, K, N), np.full(N, 2.0, np.float32))
         ok = bool(np.array_equal(ref.view(np.uint32), Y[:rows].cpu().numpy().view(np.uint32)))
         adds = T.flops(M, N, nnz)
-        print(json.dumps({"shape": name, "M": M, "K": K, "N": N, "s": s, "kernel": h.kernel_name(),
+        print(json.dumps({"shape": name, "M": M, "K": K, "N": N, "s": s, "kernel": h.call_kernel(M),
                           "kernel_ms": round(ms, 4), "step_ms": round(step_ms, 4),
                           "gflops_kernel": round(adds / (ms * 1e-3) / 1e9, 1),
                           "valu_frac": round(adds / (ms * 1e-3) / 78.64e12, 4),

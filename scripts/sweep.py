@@ -61,7 +61,7 @@ def main():
                  else T.TCSCDevice.from_blocked(*blk, K, N, a.B, device=0))
             out[f"{fmt}_register_s"] = round(time.time() - t0, 3)
             h.reserve(M)
-            for _ in range(2):
+            for _ in range(20):  # warmup incl. the GPU clock ramp (profiles/r02c_clock_ramp.txt)
                 h.gemm_torch(X, b, Y)
             torch.cuda.synchronize()
             h.set_timing(True)

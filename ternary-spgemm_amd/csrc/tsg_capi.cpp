@@ -89,7 +89,7 @@ namespace {
 
 // Largest M the automatic choice sends to the small-M (ELL) kernel
 // (profiles/r02e_small_m.jsonl: measured crossover against the jit kernel).
-constexpr int kEllAutoMaxM = 32;
+constexpr int kEllAutoMaxM = 16;
 
 struct DeviceGuard {
     int prev = -1;

@@ -74,7 +74,7 @@ EDGE = [
 @pytest.mark.parametrize("small_m", [0, 1], ids=["auto", "jit-only"])
 @pytest.mark.parametrize("M,K,N,s", EDGE)
 def test_edges_vs_oracle(tsg, oracle_mod, M, K, N, s, small_m):
-    """Ragged shapes, automatic kernel choice (the small-M kernel for M <= 32)
+    """Ragged shapes, automatic kernel choice (the small-M kernel for M <= 16)
     and the weight-compiled kernel forced for every M."""
     O = oracle_mod
     W = O.gen_ternary(K, N, s, M * 7 + K)

@@ -101,7 +101,7 @@ def test_config3_shape_small_m(tsg, oracle_mod, M):
     K, N = 4096, 16384
     arrs = tsg.gen_tcsc(K, N, 4, 42)
     h = tsg.TCSCDevice(*arrs, K, N)
-    assert h.call_kernel(M) == ("tsg_tcsc_ell_kernel" if M <= 32 else "tsg_jit_kernel")
+    assert h.call_kernel(M) == ("tsg_tcsc_ell_kernel" if M <= 16 else "tsg_jit_kernel")
     Xn = O.init_x_frac(M, K, 5)
     b = np.full(N, 2.0, np.float32)
     Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
