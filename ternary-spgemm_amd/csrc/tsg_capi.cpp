@@ -87,9 +87,14 @@ struct tsg_tcsc {
 
 namespace {
 
-// Largest M the automatic choice sends to the small-M (ELL) kernel
-// (profiles/r02e_small_m.jsonl: measured crossover against the jit kernel).
-constexpr int kEllAutoMaxM = 16;
+// Largest M the automatic choice sends to the small-M (ELL) kernel (see
+// pick_ell_variant), the variant with 8-row tiles, and the M up to which
+// 8-row tiles are used.
+constexpr int kEllAutoMaxM = 64;
+constexpr int kEllAutoMaxMChunked = 16;
+constexpr int kEllTile8 = 2;
+constexpr int kEllMidM = 32;
+static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
 
 struct DeviceGuard {
     int prev = -1;
@@ -290,13 +295,34 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
 
 // Small-M kernel choice (DESIGN.md 4 "Small M"): the sliced-ELL walk for a
 // plain-TCSC weight-compiled handle when M is small enough that the jit
-// kernel cannot fill the GPU; -1 = the jit (or rx) kernel.  Variant by M tile.
+// kernel cannot fill the GPU; -1 = the jit (or rx) kernel.  Measured on
+// configs[2]'s and configs[0]'s K, N (profiles/r02u_ell_lg.txt): up to M = 8
+// the smallest M tile that holds M; up to M = 32 tiles of 8 (2 rows per lane:
+// an 8-row chunk of K = 4096 fits LDS, one stream per column); above that the
+// largest tile whose chunk holds K.  Automatic up to M = 64 when an 8-row
+// tile holds K in one chunk (ELL 98 us vs jit 123 us at M = 64, K = 4096),
+// else up to M = 16 (K = 16384: 0.22 vs 0.55 ms).
 int pick_ell_variant(const tsg_tcsc *h, int M)
 {
     if (h->kind != tsg_tcsc::kJit || h->B || h->small_m == 1) return -1;
-    const int v = M <= tsg::kEllTileM[0] ? 0 : M <= tsg::kEllTileM[1] ? 1 : M <= tsg::kEllTileM[2] ? 2 : 3;
-    if (h->small_m == 2) return v;
-    return M <= kEllAutoMaxM ? v : -1;
+    const bool one8 = h->K <= tsg::kEllMaxC[kEllTile8];
+    if (h->small_m != 2 && M > (one8 ? kEllAutoMaxM : kEllAutoMaxMChunked)) return -1;
+    int v = 0;
+    if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
+        v = kEllTile8;
+    } else if (one8 && M > kEllMidM) {
+        v = kEllTile8;
+        for (int i = kEllTile8 + 1; i < tsg::kEllVariants; i++)
+            if (h->K <= tsg::kEllMaxC[i]) v = i;
+    } else {
+        while (v + 1 < tsg::kEllVariants && M > tsg::kEllTileM[v]) v++;
+    }
+    static const int force = [] {  // TSG_ELL_VARIANT: diagnostic sweeps only
+        const char *e = getenv("TSG_ELL_VARIANT");
+        return e ? atoi(e) : -1;
+    }();
+    if (force >= 0 && force < tsg::kEllVariants) v = force;
+    return v;
 }
 
 // Builds and uploads the ELL image of a variant.  Caller holds h->mu.
@@ -730,9 +756,13 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
         rc = ensure_jit_variant(h, pick_jit_width(h, m));
         if (rc) return rc;
     }
-    for (int v = 0; v < tsg::kEllVariants; v++) {  // the small-M images calls with M <= max_M run
-        const int lo = v == 0 ? 1 : tsg::kEllTileM[v - 1] + 1;
-        if (lo <= std::max(max_M, 1) && pick_ell_variant(h, lo) == v) {
+    // the small-M images calls with M <= max_M run: the choice only changes
+    // past an M tile or kEllMidM, so trying M = 1 and each of those + 1
+    // covers them all
+    for (int i = -1; i <= tsg::kEllVariants; i++) {
+        const int m = i < 0 ? 1 : i == tsg::kEllVariants ? kEllMidM + 1 : tsg::kEllTileM[i] + 1;
+        const int v = m <= std::max(max_M, 1) ? pick_ell_variant(h, m) : -1;
+        if (v >= 0) {
             rc = ensure_ell(h, v);
             if (rc) return rc;
         }

@@ -81,21 +81,26 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 }
 
 // Sliced-ELL entry stream of the small-M kernel (tsg_ell.hip header) for an
-// M tile of MT rows: per 16-column slice and step (pass, K chunk of C rows)
-// every column's entries in ascending k as the uint16 float index
-// (k - chunk base) * MT into the LDS chunk, padded with C * MT (the zero row) to the
-// slice's longest list rounded up to 8; blocks of 256 B = [16 columns][8 entries].
+// M tile of MT rows: per 16-column slice and step every column's entries in
+// ascending k as the uint16 float index (k - chunk base) * MT into the LDS
+// chunk, padded with C * MT (the zero row) to the slice's longest list rounded
+// up to 8; blocks of 256 B = [16 columns][8 entries].  One chunk (K <= C): ONE
+// step per slice, the +1 blocks then the -1 blocks; else a step per (pass,
+// chunk) in BaseTCSC's order (comp.h:37-63).  tab per (slice, step) =
+// {offset in blocks, n8 | n8pos << 16}: the first n8pos blocks add, the rest
+// subtract.  Block 0 is all padding (the walk reads it past a list's end).
 void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
                      int Cmax, int MT, EllImage &img)
 {
     img.C = std::min(Cmax, std::max(4, (K + 3) / 4 * 4));
     img.nch = std::max(1, (K + img.C - 1) / img.C);
-    img.steps = 2 * img.nch;
+    img.steps = img.nch == 1 ? 1 : 2 * img.nch;
     img.nslices = (N + 15) / 16;
     const int C = img.C, nch = img.nch, steps = img.steps;
+    const uint16_t pad = (uint16_t)(C * MT);
     img.tab.assign((size_t)img.nslices * steps * 2, 0u);
-    std::vector<uint16_t> e16;
-    e16.reserve((size_t)((int64_t)csp[N] + csn[N]) * 5 / 4 + (size_t)img.nslices * steps * 128);
+    std::vector<uint16_t> e16((size_t)128, pad);  // block 0: the padding block
+    e16.reserve((size_t)((int64_t)csp[N] + csn[N]) * 5 / 4 + (size_t)img.nslices * steps * 256 + 128);
     for (int sl = 0; sl < img.nslices; sl++) {
         int32_t cur[2][16], end[2][16];
         for (int c = 0; c < 16; c++) {
@@ -107,28 +112,36 @@ void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
             }
         }
         for (int step = 0; step < steps; step++) {
-            const int p = step / nch, j = step % nch;
-            const int32_t *ri = p ? rin : rip;
-            const int khi = (j + 1) * C;
-            int cnt[16], L = 0;
-            for (int c = 0; c < 16; c++) {
-                int q = cur[p][c];
-                while (q < end[p][c] && ri[q] < khi) q++;
-                cnt[c] = q - cur[p][c];
-                L = std::max(L, cnt[c]);
-            }
-            const int n8 = (L + 7) / 8;
             const size_t at = e16.size();
-            img.tab[((size_t)sl * steps + step) * 2] = (uint32_t)(at / 128);
-            img.tab[((size_t)sl * steps + step) * 2 + 1] = (uint32_t)n8;
-            e16.resize(at + (size_t)n8 * 128, (uint16_t)(C * MT));
-            for (int c = 0; c < 16; c++) {
-                for (int i = 0; i < cnt[c]; i++) {
-                    const int k = ri[cur[p][c] + i];
-                    e16[at + (size_t)(i / 8) * 128 + (size_t)c * 8 + (size_t)(i % 8)] = (uint16_t)((k - j * C) * MT);
+            uint32_t n8 = 0, n8pos = 0;
+            // the (pass, chunk) lists of this step: both passes of chunk 0 when steps == 1
+            for (int p = 0; p < 2; p++) {
+                if (steps > 1 && p != step / nch) continue;
+                const int j = steps > 1 ? step % nch : 0;
+                const int32_t *ri = p ? rin : rip;
+                const int khi = (j + 1) * C;
+                int cnt[16], L = 0;
+                for (int c = 0; c < 16; c++) {
+                    int q = cur[p][c];
+                    while (q < end[p][c] && ri[q] < khi) q++;
+                    cnt[c] = q - cur[p][c];
+                    L = std::max(L, cnt[c]);
                 }
-                cur[p][c] += cnt[c];
+                const int b8 = (L + 7) / 8;
+                const size_t base = e16.size();
+                e16.resize(base + (size_t)b8 * 128, pad);
+                for (int c = 0; c < 16; c++) {
+                    for (int i = 0; i < cnt[c]; i++) {
+                        const int k = ri[cur[p][c] + i];
+                        e16[base + (size_t)(i / 8) * 128 + (size_t)c * 8 + (size_t)(i % 8)] = (uint16_t)((k - j * C) * MT);
+                    }
+                    cur[p][c] += cnt[c];
+                }
+                n8 += (uint32_t)b8;
+                if (p == 0) n8pos = (uint32_t)b8;
             }
+            img.tab[((size_t)sl * steps + step) * 2] = (uint32_t)(at / 128);
+            img.tab[((size_t)sl * steps + step) * 2 + 1] = n8 | n8pos << 16;
         }
     }
     img.ent.assign((e16.size() + 1) / 2 + 4, 0u);

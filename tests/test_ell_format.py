@@ -1,36 +1,42 @@
 """The small-M kernel's sliced-ELL image (tsg_ell.hip), checked on the CPU
 before any GPU runs it: tsg_ell_build's image is decoded and the kernel's walk
-replayed in numpy -- per 16-column slice and step (pass, K chunk) each
+replayed in numpy -- per 16-column slice and step (one step with the +1 then
+the -1 blocks when K fits one chunk, else one per (pass, K chunk)) each
 column's uint16 entries (float indices of X^T rows of an M tile) in order,
-y = y + x in the +1 pass and y = y - x in the -1 pass, padding entries on the
-zero row -- and Y must equal the BaseTCSC oracle (comp.h:25-69) bit for bit,
-for integer and for order-sensitive non-integer X."""
+y = y + x in the blocks below n8pos and y = y - x after, padding entries on
+the zero row -- and Y must equal the BaseTCSC oracle (comp.h:25-69) bit for
+bit, for integer and for order-sensitive non-integer X."""
 import numpy as np
 import pytest
 
 
 def replay(ent, tab, C, nch, X, K, N, MT):
     M = X.shape[0]
-    steps = 2 * nch
+    steps = 1 if nch == 1 else 2 * nch
     nslices = (N + 15) // 16
     tab = tab.reshape(nslices, steps, 2)
     y = np.zeros((M, nslices * 16), np.float32)
     for st in range(steps):
-        j = st % nch
+        j = 0 if steps == 1 else st % nch
         xs = np.zeros((C + 1, M), np.float32)  # X^T chunk + the zero row
         rows = min(C, K - j * C)
         if rows > 0:
             xs[:rows] = X[:, j * C:j * C + rows].T
         for sl in range(nslices):
-            off, n8 = (int(v) for v in tab[sl, st])
+            off, w = (int(v) for v in tab[sl, st])
+            n8, n8pos = w & 0xFFFF, w >> 16
+            assert off >= 1 and n8pos <= n8
+            if steps > 1:
+                assert n8pos == (n8 if st < nch else 0)
             blk = ent[off * 128:(off + n8) * 128].reshape(n8, 16, 8)  # [i8][column][8 entries]
             for c in range(16):
                 col = sl * 16 + c
-                for u in blk[:, c, :].reshape(-1):
-                    u = int(u)
-                    assert u % MT == 0 and u // MT <= C
-                    x = xs[u // MT]
-                    y[:, col] = y[:, col] - x if st >= nch else y[:, col] + x
+                for i in range(n8):
+                    for u in blk[i, c, :]:
+                        u = int(u)
+                        assert u % MT == 0 and u // MT <= C
+                        x = xs[u // MT]
+                        y[:, col] = y[:, col] + x if i < n8pos else y[:, col] - x
     return y[:, :N]
 
 
@@ -46,8 +52,10 @@ def test_ell_replay_equals_base_tcsc(tsg, oracle_mod, M, K, N, s, Cmax, MT):
     for X in (O.init_x_int(M, K, 3), O.init_x_frac(M, K, 4)):
         Y = replay(ent, tab, C, nch, X, K, N, MT) + b
         assert np.array_equal(Y.view(np.uint32), O.base_tcsc(X, t, b).view(np.uint32))
-    # every nonzero appears once; everything else is the zero row, blocks of 8
-    used = ent[:int((tab[:, 0] + tab[:, 1]).max(initial=0)) * 128]  # the blocks (the array has tail padding)
+    # block 0 is all padding (read past a list's end); every nonzero appears
+    # once; everything else is the zero row, blocks of 8
+    assert np.all(ent[:128] == C * MT)
+    used = ent[128:int((tab[:, 0] + (tab[:, 1] & 0xFFFF)).max(initial=1)) * 128]  # (the array has tail padding)
     real = used[used != C * MT]
     assert len(real) == len(t.arrays[2]) + len(t.arrays[3])
 

@@ -1,9 +1,9 @@
 """The small-M kernel (tsg_tcsc_ell_kernel, tsg_ell.hip) on the GPU, through
 the C-ABI: forced onto every call (tcsc_hip_set_small_m(h, 2)) over the edge
-shapes of test_gpu_parity.py, every variant (M tiles of 4, 16 and 32 rows,
-several tiles), PReLU, special values and K chunking; the automatic choice;
-config 3's K and N at M = 1, 16, 64 against the oracle; graph capture after
-reserve.  Bit for bit against the BaseTCSC oracle (comp.h:25-69)."""
+shapes of test_gpu_parity.py, every variant (M tiles of 1, 4, 8, 16 and 32
+rows, several tiles, one stream or K chunks), PReLU, special values; the
+automatic choice; configs[2]'s K and N at M = 1 ... 96 against the oracle;
+configs[0] itself; graph capture after reserve.  Bit for bit against the BaseTCSC oracle (comp.h:25-69)."""
 import numpy as np
 import pytest
 
@@ -28,12 +28,16 @@ def test_edges_forced_small_m(tsg, oracle_mod, M, K, N, s):
     h.close()
 
 
-@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 16, 17, 31, 32, 33, 64, 100])
-def test_every_variant_and_tiling(tsg, oracle_mod, M):
-    """M picks the variant (tile 4 / 16 / 32); M past a tile runs several tiles.
-    K = 2300 spans several K chunks for every variant (C = 2048 / 512 / 256)."""
+@pytest.mark.parametrize("M,K", [(1, 2300), (2, 2300), (3, 2300), (4, 2300), (5, 2300), (16, 2300), (17, 2300),
+                                 (31, 2300), (32, 2300), (33, 2300), (64, 2300), (100, 2300),
+                                 (1, 20000), (3, 9000), (16, 6000), (40, 6000)])
+def test_every_variant_and_tiling(tsg, oracle_mod, M, K):
+    """M and K pick the M tile (1 / 4 / 8 / 16 / 32 rows) and the lanes per
+    column; M past a tile runs several tiles.  K = 2300 fits one LDS chunk for
+    every tile up to 16 rows (one +1/-1 stream per column); K = 6000, 9000 and
+    20000 split into K chunks (a step per pass and chunk, restaged)."""
     O = oracle_mod
-    K, N = 2300, 530
+    N = 530
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, 40 + M))
     h = tsg.TCSCDevice(*t.arrays, K, N)
     h.set_small_m(2)
@@ -92,22 +96,38 @@ def test_auto_choice_and_structural_edges(tsg, oracle_mod):
         hb.set_small_m(2)
 
 
-@pytest.mark.parametrize("M", [1, 16, 32, 64])
+@pytest.mark.parametrize("M", [1, 16, 32, 64, 96])
 def test_config3_shape_small_m(tsg, oracle_mod, M):
     """configs[2]'s K = 4096, N = 16384 at GEMV-like M (the reference sweep's
-    M list, plots/run_benchmark.py:8), automatic choice, against the oracle."""
+    M list, plots/run_benchmark.py:8), automatic choice (the small-M kernel up
+    to M = 64 at this K), against the oracle."""
     import torch
     O = oracle_mod
     K, N = 4096, 16384
     arrs = tsg.gen_tcsc(K, N, 4, 42)
     h = tsg.TCSCDevice(*arrs, K, N)
-    assert h.call_kernel(M) == ("tsg_tcsc_ell_kernel" if M <= 16 else "tsg_jit_kernel")
+    assert h.call_kernel(M) == ("tsg_tcsc_ell_kernel" if M <= 64 else "tsg_jit_kernel")
     Xn = O.init_x_frac(M, K, 5)
     b = np.full(N, 2.0, np.float32)
     Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
     rows = np.unique(np.r_[0, M // 2, M - 1])
     ref = O.base_tcsc(np.ascontiguousarray(Xn[rows]), O.TCSC(*arrs, K, N), b)
     assert _bits_eq(Y[rows], ref)
+    h.close()
+
+
+def test_config0_runs_small_m(tsg, oracle_mod):
+    """configs[0] (M = 32, K = 1024, N = 4096, s = 4; BASELINE.json) takes the
+    small-M kernel automatically (8-row tiles; 12 us vs 26 us on the jit
+    kernel, profiles/r02u_ell_lg.txt) and matches the oracle bit for bit."""
+    O = oracle_mod
+    M, K, N = 32, 1024, 4096
+    arrs = tsg.gen_tcsc(K, N, 4, 42)
+    h = tsg.TCSCDevice(*arrs, K, N)
+    assert h.call_kernel(M) == "tsg_tcsc_ell_kernel"
+    b = np.full(N, 2.0, np.float32)
+    for X in (O.init_x_int(M, K, 3), O.init_x_frac(M, K, 4)):
+        assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, O.TCSC(*arrs, K, N), b))
     h.close()
 
 
