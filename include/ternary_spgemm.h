@@ -134,12 +134,14 @@ int tcsc_hip_jit_width(const tsg_tcsc *h, int M);
 int tcsc_hip_set_jit_width(tsg_tcsc *h, int width);
 
 /* Small-M kernel (no reference counterpart; DESIGN.md 4 "Small M"): calls
- * with few rows (GEMV-like, M <= 16 by default) on a plain-TCSC handle run an
- * index-reading sliced-ELL walk (tsg_tcsc_ell_kernel) that reads X in place
- * and streams its entry stream from HBM once per M tile, instead of the
- * weight-compiled kernel.  Same results bit for bit.  mode: 0 = automatic
- * (default), 1 = never, 2 = every call (tests).  The image is built on the
- * first call that needs it (or tcsc_hip_reserve).
+ * with few rows (GEMV-like: M <= 64 when K fits an 8-row LDS chunk, else
+ * M <= 16) on a plain-TCSC handle run an index-reading sliced-ELL walk
+ * (tsg_tcsc_ell_kernel; tsg_tcsc_ell_pc_kernel, a producer/consumer split of
+ * it, for M = 1) that reads X in place and streams its entry stream from HBM
+ * once per M tile, instead of the weight-compiled kernel.  Same results bit
+ * for bit.  mode: 0 = automatic (default), 1 = never, 2 = every call, 3 =
+ * every call without the producer/consumer split (tests).  The image is built
+ * on the first call that needs it (or tcsc_hip_reserve).
  * tcsc_hip_call_kernel: the kernel a call with M rows launches. */
 int tcsc_hip_set_small_m(tsg_tcsc *h, int mode);
 const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M);

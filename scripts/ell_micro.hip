@@ -40,6 +40,7 @@ __device__ __forceinline__ uint32_t mad_hi(uint32_t w, uint32_t base)
 }
 
 template <int MODE> struct Rows { static constexpr int R = MODE == 3 ? 4 : MODE == 4 ? 2 : 1; };
+// mode 5: mode 1 + ONE s_waitcnt lgkmcnt(8) per block before its adds
 
 template <int MODE>
 __device__ __forceinline__ void load8(float (&x)[8][Rows<MODE>::R], const uint4 e, const float *xs, uint32_t base)
@@ -110,6 +111,10 @@ __global__ __launch_bounds__(64) void walk(const uint4 *__restrict__ ent, int nb
                 else load8<MODE>(x0, q[d + 1], xs, base);
             }
             if (SB) __builtin_amdgcn_sched_barrier(0);  // block d+1's reads stay ahead of block d's adds
+            if (MODE == 5) {
+                if (d + 1 < D) __builtin_amdgcn_s_waitcnt(0xC87F);  // lgkmcnt(8)
+                else __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0)
+            }
             add8<MODE>(y, d % 2 == 0 ? x0 : x1);
             if (SB) __builtin_amdgcn_sched_barrier(0);
             q[d] = p[(size_t)min(i + D + d, last) * ncol];
@@ -244,6 +249,161 @@ void run_dpp(const uint4 *dent, int nblk, float *dout, unsigned long long *dcyc,
     CK(hipEventDestroy(b));
 }
 
+// Producer / consumer: P producer waves gather the X values of the next phase
+// (E entries of each of 64 columns) into an LDS buffer in chain order while
+// the consumer wave (lane = column) adds the current phase's from the other
+// buffer, 4 per ds_read_b128; one barrier per phase.
+// a workgroup barrier that orders LDS only (global loads stay in flight)
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int E>
+__global__ __launch_bounds__(64 * (1 + E / 8)) void walk_pc(const uint4 *__restrict__ ent, int nblk, float *out,
+                                                            unsigned long long *cyc)
+{
+    constexpr int P = E / 8, D = 16;  // producer waves; phases of index blocks in flight per producer lane
+    __shared__ __attribute__((aligned(16))) float xs[4096];
+    __shared__ __attribute__((aligned(16))) float4 buf[2][E / 4][64];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int i = tid; i < 4096; i += 64 * (1 + P)) xs[i] = (float)(i % 97) * 0.25f;
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_f *)xs;
+    const int nph = nblk * 8 / E;
+    const int col0 = blockIdx.x * 64;
+    __syncthreads();
+    unsigned long long t0 = 0, t1 = 0;
+    if (wave == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (wave == 0) {  // consumer
+        float y = 0.0f;
+        lds_barrier();  // phase 0 filled
+        for (int ph = 0; ph < nph; ph++) {
+            const float4 *bp = &buf[ph & 1][0][lane];
+#pragma unroll
+            for (int q4 = 0; q4 < E / 4; q4++) {
+                const float4 v = bp[q4 * 64];
+                y += v.x; y += v.y; y += v.z; y += v.w;
+            }
+            lds_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        out[col0 + lane] = y;
+        if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+    } else {  // producer: column lane, block j of each phase
+        const int j = wave - 1;
+        const uint4 *p = ent + (size_t)j * 65536 + col0 + lane;  // block ph * P + j of the column: lanes contiguous
+        uint4 q[D];
+#pragma unroll
+        for (int d = 0; d < D; d++) q[d] = p[(size_t)min(d, nph - 1) * P * 65536];
+        auto fill = [&](int ph, const uint4 e) {
+            const uint32_t w[4] = {e.x, e.y, e.z, e.w};
+            float x[8];
+#pragma unroll
+            for (int h = 0; h < 8; h++)
+                x[h] = *(lds_f *)(uintptr_t)((h & 1) ? mad_hi(w[h >> 1], base) : mad_lo(w[h >> 1], base));
+            buf[ph & 1][2 * j][lane] = make_float4(x[0], x[1], x[2], x[3]);
+            buf[ph & 1][2 * j + 1][lane] = make_float4(x[4], x[5], x[6], x[7]);
+        };
+        fill(0, q[0]);
+        q[0] = p[(size_t)min(D, nph - 1) * P * 65536];
+        lds_barrier();
+        // branch-free: phase g + d + 1 from slot (d + 1) % D (the last fill,
+        // phase nph, lands in the buffer nobody reads again)
+        for (int g = 0; g < nph; g += D) {
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                const int ph = g + d + 1;
+                fill(ph, q[(d + 1) % D]);
+                q[(d + 1) % D] = p[(size_t)min(ph + D, nph - 1) * P * 65536];
+                lds_barrier();
+            }
+        }
+    }
+}
+
+template <int E>
+void run_pc(const uint4 *dent, int nblk, float *dout, unsigned long long *dcyc, int grid)
+{
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int w = 0; w < 30; w++) hipLaunchKernelGGL(walk_pc<E>, dim3(grid), dim3(64 * (1 + E / 8)), 0, 0, dent, nblk, dout, dcyc);
+    CK(hipEventRecord(a));
+    const int reps = 20;
+    for (int w = 0; w < reps; w++) hipLaunchKernelGGL(walk_pc<E>, dim3(grid), dim3(64 * (1 + E / 8)), 0, 0, dent, nblk, dout, dcyc);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<unsigned long long> c(grid);
+    CK(hipMemcpy(c.data(), dcyc, grid * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    double avg = 0;
+    for (auto v : c) avg += (double)v;
+    avg /= grid;
+    const double entries = nblk * 8.0;
+    std::printf("pc E %2d grid %5d (%6d columns) entries/col %5.0f: kernel %.2f us, %.2f ns/entry, stamp %.2f ticks/entry\n",
+                E, grid, grid * 64, entries, ms * 1000.0 / reps, ms * 1e6 / reps / entries, avg / entries);
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+}
+
+// The consumer's floor: CH independent chains per lane, fed 4 values per
+// ds_read_b128 from a lane-contiguous LDS buffer (no gather, no barrier).
+template <int CH>
+__global__ __launch_bounds__(64) void chain_floor(int n4, float *out, unsigned long long *cyc)
+{
+    __shared__ __attribute__((aligned(16))) float4 buf[64][64];
+    const int lane = threadIdx.x;
+    for (int i = 0; i < 64; i++) buf[i][lane] = make_float4(lane, i, 0.5f, 0.25f);
+    __syncthreads();
+    float y[CH];
+#pragma unroll
+    for (int c = 0; c < CH; c++) y[c] = 0.0f;
+    unsigned long long t0, t1;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < n4; i += 16) {
+        float4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = buf[(i + u) & 63][lane];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            if constexpr (CH == 1) { y[0] += v[u].x; y[0] += v[u].y; y[0] += v[u].z; y[0] += v[u].w; }
+            else if constexpr (CH == 2) { y[0] += v[u].x; y[1] += v[u].y; y[0] += v[u].z; y[1] += v[u].w; }
+            else { y[0] += v[u].x; y[1] += v[u].y; y[2] += v[u].z; y[3] += v[u].w; }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    float s = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CH; c++) s += y[c];
+    out[blockIdx.x * 64 + lane] = s;
+    if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int CH>
+void run_floor(float *dout, unsigned long long *dcyc)
+{
+    const int n4 = 1024;  // 4096 adds per lane
+    for (int w = 0; w < 10; w++) hipLaunchKernelGGL(chain_floor<CH>, dim3(4), dim3(64), 0, 0, n4, dout, dcyc);
+    CK(hipDeviceSynchronize());
+    unsigned long long c[4];
+    CK(hipMemcpy(c, dcyc, sizeof(c), hipMemcpyDeviceToHost));
+    std::printf("chain floor: %d chains per lane, %.2f ticks per add (%.2f per add of one chain)\n", CH,
+                (double)c[0] / (4.0 * n4), (double)c[0] / (4.0 * n4) * CH);
+}
+
 int main()
 {
     const int ncol = 1024 * 64;  // up to 1024 waves
@@ -272,16 +432,19 @@ int main()
     CK(hipMemcpy(d2, h2.data(), h.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d4, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     // DPP chains: 1024 entries per column; d1 holds >= 4096 * 64 * 128 * 4 words
-    for (int grid : {4, 256, 1024, 4096}) {
-        run_dpp<16>(d1, 8, dout, dcyc, grid);
+    run_floor<1>(dout, dcyc);
+    run_floor<2>(dout, dcyc);
+    run_floor<4>(dout, dcyc);
+    for (int grid : {4, 256, 1024}) {
+        run_pc<16>(d1, 128, dout, dcyc, grid);
+        run_pc<32>(d1, 128, dout, dcyc, grid);
+        run<1>(d1, 128, ncol, dout, dcyc, grid);
+        run<5>(d1, 128, ncol, dout, dcyc, grid);
+        run<1, true, 16>(d1, 128, ncol, dout, dcyc, grid);
+        run<5, true, 16>(d1, 128, ncol, dout, dcyc, grid);
         if (grid <= 1024) run_dpp<4>(d1, 32, dout, dcyc, grid);
     }
-    for (int grid : {4, 256, 1024}) {
-        run<1, true, 16>(d1, 128, ncol, dout, dcyc, grid);
-        run<1, true, 32>(d1, 128, ncol, dout, dcyc, grid);
-        run<3, true, 16>(d4, 128, ncol, dout, dcyc, grid);
-        run<4, true, 32>(d2, 128, ncol, dout, dcyc, grid);
-    }
+    if (getenv("ELL_MICRO_ALL") == nullptr) return 0;
     for (int grid : {4, 256, 1024}) {
         for (int nb : {128}) {
             run<0, false>(d1, nb, ncol, dout, dcyc, grid);

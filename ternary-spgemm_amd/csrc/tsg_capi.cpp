@@ -60,7 +60,7 @@ struct tsg_tcsc {
         bool ready = false;
     };
     EllVariant ell[tsg::kEllVariants];
-    int small_m = 0;                      // tcsc_hip_set_small_m: 0 auto, 1 never, 2 always (plain TCSC only)
+    int small_m = 0;                      // tcsc_hip_set_small_m: 0 auto, 1 never, 2 always, 3 always w/o pc (plain TCSC only)
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
     float *d_work = nullptr;              // X^T [Kp][Mp]
@@ -306,7 +306,7 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
 {
     if (h->kind != tsg_tcsc::kJit || h->B || h->small_m == 1) return -1;
     const bool one8 = h->K <= tsg::kEllMaxC[kEllTile8];
-    if (h->small_m != 2 && M > (one8 ? kEllAutoMaxM : kEllAutoMaxMChunked)) return -1;
+    if (h->small_m < 2 && M > (one8 ? kEllAutoMaxM : kEllAutoMaxMChunked)) return -1;
     int v = 0;
     if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
         v = kEllTile8;
@@ -323,6 +323,22 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     }();
     if (force >= 0 && force < tsg::kEllVariants) v = force;
     return v;
+}
+
+// The producer/consumer walk (tsg_tcsc_ell_pc_kernel) for the 1-row tile
+// when K fits one chunk: few chains, each latency-bound (M = 1: 15.6 vs 20.6
+// us at K = 4096, N = 16384; profiles/r02x_ell_pc.txt).  TSG_ELL_PC=0 turns it
+// off (diagnostic A/B).
+bool use_ell_pc(const tsg_tcsc *h, int v)
+{
+    static const bool on = [] {
+        const char *e = getenv("TSG_ELL_PC");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || h->small_m == 3 || v != 0 || h->K > tsg::kEllMaxC[v]) return false;
+    const int C = std::min(tsg::kEllMaxC[v], std::max(4, (h->K + 3) / 4 * 4));  // build_ell_image's chunk
+    const size_t lds = tsg::ell_pc_lds_bytes(v, C);
+    return lds > 0 && lds <= tsg::kLdsBytes;
 }
 
 // Builds and uploads the ELL image of a variant.  Caller holds h->mu.
@@ -382,8 +398,11 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
             HIP_TRY(hipEventRecord(h->ev0[slot], s));
         }
         const tsg_tcsc::EllVariant &e = h->ell[ev];
-        if (tsg::launch_tcsc_ell(ev, dX, e.d_ent, e.d_tab, db, dalpha, dY, M, N, K, e.img.C, e.img.nch,
-                                 prelu ? 1 : 0, s) != 0)
+        const int lrc = use_ell_pc(h, ev) ? tsg::launch_tcsc_ell_pc(ev, dX, e.d_ent, e.d_tab, db, dalpha, dY, M, N, K,
+                                                                    e.img.C, e.img.nch, prelu ? 1 : 0, s)
+                                          : tsg::launch_tcsc_ell(ev, dX, e.d_ent, e.d_tab, db, dalpha, dY, M, N, K,
+                                                                 e.img.C, e.img.nch, prelu ? 1 : 0, s);
+        if (lrc != 0)
             return fail(TSG_ERR_HIP, std::string("small-M kernel launch: ") + hipGetErrorString(hipGetLastError()));
         if (slot >= 0) {
             HIP_TRY(hipEventRecord(h->ev1[slot], s));
@@ -790,8 +809,10 @@ extern "C" int tcsc_hip_jit_width(const tsg_tcsc *h, int M)
 extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)
 {
     if (!h) return fail(TSG_ERR_ARG, "null handle");
-    if (mode < 0 || mode > 2) return fail(TSG_ERR_ARG, "tcsc_hip_set_small_m: expected 0 (auto), 1 (never) or 2 (always)");
-    if (mode == 2 && (h->kind != tsg_tcsc::kJit || h->B))
+    if (mode < 0 || mode > 3)
+        return fail(TSG_ERR_ARG, "tcsc_hip_set_small_m: expected 0 (auto), 1 (never), 2 (always) or 3 (always, "
+                                 "without the producer/consumer walk)");
+    if (mode >= 2 && (h->kind != tsg_tcsc::kJit || h->B))
         return fail(TSG_ERR_ARG, "tcsc_hip_set_small_m: the small-M kernel computes plain TCSC (BaseTCSC) only");
     std::lock_guard<std::mutex> lk(h->mu);
     h->small_m = mode;
@@ -801,8 +822,9 @@ extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)
 extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)
 {
     if (!h) return "";
-    return pick_ell_variant(h, M) >= 0 ? "tsg_tcsc_ell_kernel"
-           : h->kind == tsg_tcsc::kJit ? "tsg_jit_kernel" : "tsg_tcsc_rx_kernel";
+    const int ev = pick_ell_variant(h, M);
+    if (ev >= 0) return use_ell_pc(h, ev) ? "tsg_tcsc_ell_pc_kernel" : "tsg_tcsc_ell_kernel";
+    return h->kind == tsg_tcsc::kJit ? "tsg_jit_kernel" : "tsg_tcsc_rx_kernel";
 }
 
 extern "C" int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K)

@@ -165,6 +165,61 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t n)
     return __builtin_amdgcn_readfirstlane(n);
 }
 
+// Stage X^T[chunk at kc][MT rows from m0] into xs ([C][MT], row-major by k)
+// with NT threads: a thread loads 4 consecutive k of one row m (16 B when
+// aligned) and writes them to 4 LDS rows; consecutive threads take
+// consecutive m, so the LDS writes hit consecutive banks.  SB unconditional
+// loads from clamped in-range addresses go out before their masked stores
+// (no branch between them, so no wait per load).  Rows past M and k past K
+// are +0.
+template <int MT, int NT, int SB>
+__device__ __forceinline__ void ell_stage(float *xs, const float *__restrict__ X, int M, int K, int m0, int kc, int C,
+                                          int tid, bool vec)
+{
+    const int per = C / 4 * MT;
+    if (vec) {
+        for (int i0 = tid; i0 < per; i0 += SB * NT) {
+            float4 v[SB];
+#pragma unroll
+            for (int u = 0; u < SB; u++) {
+                const int i = i0 + u * NT;
+                const int mm = i % MT, r4 = (i / MT) * 4, m = m0 + mm, k = kc + r4;
+                const bool in = i < per && m < M && k + 3 < K;
+                v[u] = *reinterpret_cast<const float4 *>(X + (in ? (size_t)m * K + k : 0));
+            }
+#pragma unroll
+            for (int u = 0; u < SB; u++) {
+                const int i = i0 + u * NT;
+                const int mm = i % MT, r4 = (i / MT) * 4, m = m0 + mm, k = kc + r4;
+                const bool in = i < per && m < M && k + 3 < K;
+                const float4 w = in ? v[u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (i < per) {
+                    xs[(r4 + 0) * MT + mm] = w.x;
+                    xs[(r4 + 1) * MT + mm] = w.y;
+                    xs[(r4 + 2) * MT + mm] = w.z;
+                    xs[(r4 + 3) * MT + mm] = w.w;
+                }
+            }
+        }
+    } else {
+        for (int i = tid; i < per; i += NT) {
+            const int mm = i % MT, r4 = (i / MT) * 4, m = m0 + mm, k = kc + r4;
+            float4 w = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (m < M) {
+                const float *xr = X + (size_t)m * K + k;
+                if (k < K) w.x = xr[0];
+                if (k + 1 < K) w.y = xr[1];
+                if (k + 2 < K) w.z = xr[2];
+                if (k + 3 < K) w.w = xr[3];
+            }
+            xs[(r4 + 0) * MT + mm] = w.x;
+            xs[(r4 + 1) * MT + mm] = w.y;
+            xs[(r4 + 2) * MT + mm] = w.z;
+            xs[(r4 + 3) * MT + mm] = w.w;
+        }
+    }
+}
+
 }  // namespace
 
 template <int LG, int RPL, int WPG, bool PRELU>
@@ -213,54 +268,7 @@ __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
         const int j = steps == 1 ? 0 : step % nch, kc = j * C;
         if (step == 0 || steps > 1) {
             __syncthreads();  // previous chunk's reads are done
-            // stage X^T[chunk j] -- a thread loads 4 consecutive k of one row m
-            // (16 B when aligned) and writes them to 4 LDS rows; consecutive
-            // threads take consecutive m, so the LDS writes hit consecutive
-            // banks.
-            const int per = C / 4 * MT;
-            if (vec) {
-                for (int i0 = tid; i0 < per; i0 += SB * WPG * 64) {
-                    // SB unconditional loads from clamped in-range addresses
-                    // (no branch between them, so no wait), then masked stores
-                    float4 v[SB];
-#pragma unroll
-                    for (int u = 0; u < SB; u++) {
-                        const int i = i0 + u * WPG * 64;
-                        const int mm = i % MT, r4 = (i / MT) * 4, m = m0 + mm, k = kc + r4;
-                        const bool in = i < per && m < M && k + 3 < K;
-                        v[u] = *reinterpret_cast<const float4 *>(X + (in ? (size_t)m * K + k : 0));
-                    }
-#pragma unroll
-                    for (int u = 0; u < SB; u++) {
-                        const int i = i0 + u * WPG * 64;
-                        const int mm = i % MT, r4 = (i / MT) * 4, m = m0 + mm, k = kc + r4;
-                        const bool in = i < per && m < M && k + 3 < K;
-                        const float4 w = in ? v[u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        if (i < per) {
-                            xs[(r4 + 0) * MT + mm] = w.x;
-                            xs[(r4 + 1) * MT + mm] = w.y;
-                            xs[(r4 + 2) * MT + mm] = w.z;
-                            xs[(r4 + 3) * MT + mm] = w.w;
-                        }
-                    }
-                }
-            } else {
-                for (int i = tid; i < per; i += WPG * 64) {
-                    const int mm = i % MT, r4 = (i / MT) * 4, m = m0 + mm, k = kc + r4;
-                    float4 w = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                    if (m < M) {
-                        const float *xr = X + (size_t)m * K + k;
-                        if (k < K) w.x = xr[0];
-                        if (k + 1 < K) w.y = xr[1];
-                        if (k + 2 < K) w.z = xr[2];
-                        if (k + 3 < K) w.w = xr[3];
-                    }
-                    xs[(r4 + 0) * MT + mm] = w.x;
-                    xs[(r4 + 1) * MT + mm] = w.y;
-                    xs[(r4 + 2) * MT + mm] = w.z;
-                    xs[(r4 + 3) * MT + mm] = w.w;
-                }
-            }
+            ell_stage<MT, WPG * 64, SB>(xs, X, M, K, m0, kc, C, tid, vec);
             __syncthreads();
         }
         ell_walk<RPL, D>(y, q, e0, off, n8, n8pos, nmax, base);
@@ -275,6 +283,181 @@ __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
         float v = y[r] + bn;                         // comp.h:63
         if (PRELU) v = (v > 0) ? v : an * v;         // comp_prelu.h:57-67
         Y[(size_t)m * N + n] = v;
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// tsg_tcsc_ell_pc_kernel: the same image and order for very few chains (M = 1,
+// K in one LDS chunk), where each Y[m,n] chain's latency, not throughput,
+// bounds the walk (~26 cycles per entry for a wave that also gathers; a lone
+// dependent fma chain fed by ds_read_b128 runs at ~7, profiles/r02q_ell_micro.txt).  A workgroup owns 64 columns x MT rows = 64 MT chains and
+// splits the work: MT consumer waves (a lane = a chain) do nothing but the
+// chain -- y = fma(x, +-1, y), x read 4 at a time with ds_read_b128 one phase
+// ahead -- while MT * E / 8 producer waves (a lane = one chain's index block
+// of a phase) gather the next phases' X values (v_mad_u32_u16 address, one LDS
+// read per entry) into a 3-slot LDS ring laid out in chain order.  A phase =
+// E entries of every chain; one LDS-only barrier per phase (index-block loads
+// stay in flight across it).  Slot ph % 3 holds phase ph: producers fill phase
+// k + 2 while the consumers add phase k and read phase k + 1.
+namespace {
+
+__device__ __forceinline__ void lds_barrier()
+{
+    // nothing moves across it: the scheduler would otherwise hoist later
+    // phases' address math (and with it the waits for their index blocks)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int MT, int E>
+struct PcShape {
+    static constexpr int CH = 64 * MT;  // chains: 64 columns x MT rows (chain = column * MT + row)
+    static constexpr int CW = MT;       // consumer waves
+    static constexpr int NB = E / 8;    // index blocks per column per phase
+    static constexpr int PW = NB;       // producer waves (a lane = a column's block: all MT rows)
+    static constexpr int NT = 64 * (CW + PW);
+    static constexpr int D = 16;        // phases of index blocks in flight per producer lane
+};
+
+}  // namespace
+
+template <int MT, int E, bool PRELU>
+__global__ __launch_bounds__(64 * (MT + E / 8)) void tsg_tcsc_ell_pc_kernel(
+    const float *__restrict__ X, const uint4 *__restrict__ ent, const uint2 *__restrict__ tab,
+    const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N, int K,
+    int C, int nsg)
+{
+    using S = PcShape<MT, E>;
+    static_assert(S::NT == 64 * (MT + E / 8), "launch bounds");
+    constexpr int CH = S::CH, CW = S::CW, NB = S::NB, D = S::D;
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // [(C + 1)][MT], then float4 ring[3][E / 4][CH]
+    float4 *ring = reinterpret_cast<float4 *>(xs + ((C + 1) * MT + 3) / 4 * 4);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sg = blockIdx.x % nsg, mt = blockIdx.x / nsg;
+    const int m0 = mt * MT;
+    const int nslices = (N + 15) / 16;
+    const bool consumer = wave < CW;
+    const int pj = consumer ? 0 : wave - CW;          // a producer's block within the phase
+    const int ch = consumer ? wave * 64 + lane : 0;   // a consumer lane's chain
+    const int n = sg * 64 + (consumer ? ch / MT : lane), r = consumer ? ch % MT : 0;  // its column (and row)
+    const int slice = n >> 4;
+    uint32_t off = 0, n8 = 0, n8pos = 0;
+    if (slice < nslices) {
+        const uint2 t = tab[slice];
+        off = t.x;
+        n8 = t.y & 0xffffu;
+        n8pos = t.y >> 16;
+    }
+    // phases: the longest list of the workgroup's 4 slices, in blocks of NB
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int sl = sg * 4 + i;
+        if (sl < nslices) nmax = max(nmax, tab[sl].y & 0xffffu);
+    }
+    const int nph = (int)((nmax + NB - 1) / NB);
+    const uint4 *e0 = ent + (n & 15);
+
+    // a producer's index blocks first (they travel while X is staged)
+    uint4 q[D];
+    auto load = [&](int ph) {
+        const uint32_t bl = (uint32_t)(ph * NB + pj);
+        return e0[bl < n8 ? (off + bl) * 16 : 0];
+    };
+    if (!consumer) {
+#pragma unroll
+        for (int d = 0; d < D; d++) q[d] = load(d);
+    }
+    for (int i = tid; i < MT; i += S::NT) xs[C * MT + i] = 0.0f;  // the zero row
+    const bool vec = K >= 4 && (K & 3) == 0 && ((((uintptr_t)X) & 15) == 0);
+    ell_stage<MT, S::NT, 8>(xs, X, M, K, m0, 0, C, tid, vec);
+    lds_barrier();
+
+    if (consumer) {
+        __builtin_amdgcn_s_setprio(3);  // the chain is the critical path
+        float y = 0.0f;                 // comp.h:41
+        float4 va[E / 4], vb[E / 4];
+        auto read = [&](float4(&v)[E / 4], int ph) {
+            const float4 *src = ring + (size_t)(ph % 3) * (E / 4) * CH + ch;
+#pragma unroll
+            for (int q4 = 0; q4 < E / 4; q4++) v[q4] = src[q4 * CH];
+        };
+        auto chain = [&](const float4(&v)[E / 4], int ph) {
+#pragma unroll
+            for (int q4 = 0; q4 < E / 4; q4++) {
+                const float sg1 = (uint32_t)(ph * NB + q4 / 2) < n8pos ? 1.0f : -1.0f;  // +1 / -1 block
+                y = __builtin_fmaf(v[q4].x, sg1, y);
+                y = __builtin_fmaf(v[q4].y, sg1, y);
+                y = __builtin_fmaf(v[q4].z, sg1, y);
+                y = __builtin_fmaf(v[q4].w, sg1, y);
+            }
+        };
+        lds_barrier();  // phases 0 and 1 are in the ring
+        read(va, 0);
+        for (int k = 0; k < nph; k += 2) {
+            read(vb, k + 1);
+            chain(va, k);
+            lds_barrier();
+            if (k + 1 >= nph) break;
+            read(va, k + 2);
+            chain(vb, k + 1);
+            lds_barrier();
+        }
+        if (n >= N || m0 + r >= M) return;
+        float v = y + b[n];                          // comp.h:63
+        if (PRELU) v = (v > 0) ? v : alpha[n] * v;   // comp_prelu.h:57-67
+        Y[(size_t)(m0 + r) * N + n] = v;
+    } else {
+        const uint32_t base = (uint32_t)(uintptr_t)(lds_f *)xs;
+        // the block's 8 entries, all MT rows each (one LDS read per entry),
+        // written as 4-entry runs of each of the column's MT chains
+        auto fill = [&](int ph, const uint4 e) {
+            const uint32_t w[4] = {e.x, e.y, e.z, e.w};
+            float x[8][MT];
+#pragma unroll
+            for (int h = 0; h < 8; h++) {
+                const uint32_t a = (h & 1) ? ent_addr_hi(w[h >> 1], base) : ent_addr_lo(w[h >> 1], base);
+                if constexpr (MT == 4) {
+                    const v4f v = *(lds_f4 *)(uintptr_t)a;
+                    x[h][0] = v.x; x[h][1] = v.y; x[h][2] = v.z; x[h][3] = v.w;
+                } else {
+                    x[h][0] = *(lds_f *)(uintptr_t)a;
+                }
+            }
+            float4 *dst = ring + ((size_t)(ph % 3) * (E / 4) + 2 * pj) * CH + lane * MT;
+#pragma unroll
+            for (int rr = 0; rr < MT; rr++) {
+                dst[rr] = make_float4(x[0][rr], x[1][rr], x[2][rr], x[3][rr]);
+                dst[CH + rr] = make_float4(x[4][rr], x[5][rr], x[6][rr], x[7][rr]);
+            }
+        };
+        fill(0, q[0]);
+        q[0] = load(D);
+        fill(1, q[1]);
+        q[1] = load(D + 1);
+        lds_barrier();
+        // phase k + 2 during phase k: whole groups of D refill their slots
+        // (no exit branch between a load and its use), the rest comes from
+        // the ring with no loads
+        int k = 0;
+        for (; k + D <= nph; k += D) {
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                fill(k + d + 2, q[(d + 2) % D]);
+                q[(d + 2) % D] = load(k + d + 2 + D);
+                lds_barrier();
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            if (k + d >= nph) break;
+            fill(k + d + 2, q[(d + 2) % D]);
+            lds_barrier();
+        }
     }
 }
 
@@ -333,7 +516,50 @@ int pick_lg(int dflt)
     return env > 0 ? env : dflt;
 }
 
+template <int MT, int E>
+constexpr size_t pc_lds(int C)
+{
+    return ((size_t)((C + 1) * MT + 3) / 4 * 4) * sizeof(float) + (size_t)3 * (E / 4) * PcShape<MT, E>::CH * 16;
+}
+
+template <int MT, int E>
+int launch_pc_t(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
+                int M, int N, int K, int C, int prelu, hipStream_t s)
+{
+    using S = PcShape<MT, E>;
+    const int nsg = (N + 63) / 64;
+    const int mtiles = (M + MT - 1) / MT;
+    const size_t lds = pc_lds<MT, E>(C);
+    const dim3 grid((unsigned)(nsg * mtiles)), block(S::NT);
+    if (prelu)
+        hipLaunchKernelGGL((tsg_tcsc_ell_pc_kernel<MT, E, true>), grid, block, lds, s, X, ent, tab, b, alpha, Y, M, N,
+                           K, C, nsg);
+    else
+        hipLaunchKernelGGL((tsg_tcsc_ell_pc_kernel<MT, E, false>), grid, block, lds, s, X, ent, tab, b, alpha, Y, M, N,
+                           K, C, nsg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 }  // namespace
+
+// 1-row tiles only: with 4 rows the ring's extra write and read of every row
+// value make the walk LDS-bound (39 vs 22.5 us at M = 4, K = 4096, N = 16384;
+// profiles/r02x_ell_pc.txt)
+size_t ell_pc_lds_bytes(int variant, int C)
+{
+    return variant == 0 ? pc_lds<1, 32>(C) : 0;
+}
+
+int launch_tcsc_ell_pc(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
+                       const float *alpha, float *Y, int M, int N, int K, int C, int nch, int prelu, void *stream)
+{
+    // one stream per column, X chunk + ring within a workgroup's LDS
+    if (nch != 1 || ell_pc_lds_bytes(variant, C) == 0 || ell_pc_lds_bytes(variant, C) > kLdsBytes) return -2;
+    hipStream_t s = (hipStream_t)stream;
+    const uint4 *e = reinterpret_cast<const uint4 *>(ent);
+    const uint2 *t = reinterpret_cast<const uint2 *>(tab);
+    return launch_pc_t<1, 32>(X, e, t, b, alpha, Y, M, N, K, C, prelu, s);  // 1 consumer + 4 producer waves
+}
 
 int launch_tcsc_ell(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
                     const float *alpha, float *Y, int M, int N, int K, int C, int nch, int prelu, void *stream)

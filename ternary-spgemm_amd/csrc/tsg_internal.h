@@ -142,6 +142,13 @@ void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                      int Cmax, int MT, EllImage &img);
 int launch_tcsc_ell(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
                     const float *alpha, float *Y, int M, int N, int K, int C, int nch, int prelu, void *stream);
+// the producer/consumer walk (tsg_tcsc_ell_pc_kernel) of variant 0 (M = 1) when
+// K fits one chunk and the chunk plus its LDS ring fit kLdsBytes
+// (ell_pc_lds_bytes; 0 = no such variant); -2 = not available for this image
+constexpr size_t kLdsBytes = 160 * 1024;
+size_t ell_pc_lds_bytes(int variant, int C);
+int launch_tcsc_ell_pc(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
+                       const float *alpha, float *Y, int M, int N, int K, int C, int nch, int prelu, void *stream);
 
 // B = 0: plain TCSC; B > 0: BlockedTCSC<B> arrays ((K/B)*N + 1 column starts)
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,

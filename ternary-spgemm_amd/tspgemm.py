@@ -498,7 +498,8 @@ class TCSCDevice:
         _check(lib().tcsc_hip_set_jit_width(self._h, width), "tcsc_hip_set_jit_width")
 
     def set_small_m(self, mode: int) -> None:
-        """Small-M kernel: 0 = automatic (default), 1 = never, 2 = every call."""
+        """Small-M kernel: 0 = automatic (default), 1 = never, 2 = every call,
+        3 = every call without the producer/consumer walk (M <= 4)."""
         _check(lib().tcsc_hip_set_small_m(self._h, mode), "tcsc_hip_set_small_m")
 
     def call_kernel(self, M: int) -> str:

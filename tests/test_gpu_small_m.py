@@ -1,5 +1,7 @@
-"""The small-M kernel (tsg_tcsc_ell_kernel, tsg_ell.hip) on the GPU, through
-the C-ABI: forced onto every call (tcsc_hip_set_small_m(h, 2)) over the edge
+"""The small-M kernels (tsg_tcsc_ell_kernel and, for M = 1, its
+producer/consumer split tsg_tcsc_ell_pc_kernel; tsg_ell.hip) on the GPU,
+through the C-ABI: forced onto every call (tcsc_hip_set_small_m(h, 2); 3 =
+without the producer/consumer split) over the edge
 shapes of test_gpu_parity.py, every variant (M tiles of 1, 4, 8, 16 and 32
 rows, several tiles, one stream or K chunks), PReLU, special values; the
 automatic choice; configs[2]'s K and N at M = 1 ... 96 against the oracle;
@@ -11,15 +13,24 @@ from test_gpu_parity import EDGE, _bits_eq
 
 pytestmark = pytest.mark.gpu
 
+SMALL = ("tsg_tcsc_ell_kernel", "tsg_tcsc_ell_pc_kernel")
 
+
+def _small_kernel(M, K, mode):
+    """The kernel tcsc_hip_set_small_m(mode) sends a call with M rows to."""
+    # M = 1 with K within the 1-row tile's LDS chunk (tsg_internal.h kEllMaxC)
+    return "tsg_tcsc_ell_pc_kernel" if mode == 2 and M == 1 and K <= 16380 else "tsg_tcsc_ell_kernel"
+
+
+@pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("M,K,N,s", EDGE)
-def test_edges_forced_small_m(tsg, oracle_mod, M, K, N, s):
+def test_edges_forced_small_m(tsg, oracle_mod, M, K, N, s, mode):
     O = oracle_mod
     W = O.gen_ternary(K, N, s, M * 7 + K)
     t = O.tcsc_encode(W)
     h = tsg.TCSCDevice(*t.arrays, K, N)
-    h.set_small_m(2)
-    assert h.call_kernel(M) == "tsg_tcsc_ell_kernel"
+    h.set_small_m(mode)
+    assert h.call_kernel(M) == _small_kernel(M, K, mode)
     b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
     alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
     for X in (O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)):
@@ -30,8 +41,9 @@ def test_edges_forced_small_m(tsg, oracle_mod, M, K, N, s):
 
 @pytest.mark.parametrize("M,K", [(1, 2300), (2, 2300), (3, 2300), (4, 2300), (5, 2300), (16, 2300), (17, 2300),
                                  (31, 2300), (32, 2300), (33, 2300), (64, 2300), (100, 2300),
-                                 (1, 20000), (3, 9000), (16, 6000), (40, 6000)])
-def test_every_variant_and_tiling(tsg, oracle_mod, M, K):
+                                 (1, 20000), (1, 16380), (3, 9000), (16, 6000), (40, 6000)])
+@pytest.mark.parametrize("mode", [2, 3])
+def test_every_variant_and_tiling(tsg, oracle_mod, M, K, mode):
     """M and K pick the M tile (1 / 4 / 8 / 16 / 32 rows) and the lanes per
     column; M past a tile runs several tiles.  K = 2300 fits one LDS chunk for
     every tile up to 16 rows (one +1/-1 stream per column); K = 6000, 9000 and
@@ -40,7 +52,8 @@ def test_every_variant_and_tiling(tsg, oracle_mod, M, K):
     N = 530
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, 40 + M))
     h = tsg.TCSCDevice(*t.arrays, K, N)
-    h.set_small_m(2)
+    h.set_small_m(mode)
+    assert h.call_kernel(M) == _small_kernel(M, K, mode)
     b = np.linspace(-3, 3, N).astype(np.float32)
     X = O.init_x_frac(M, K, M)
     assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b)), M
@@ -55,11 +68,13 @@ def test_special_values_small_m(tsg, oracle_mod):
     h = tsg.TCSCDevice(*t.arrays, K, N)
     h.set_small_m(2)
     alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
-    for M, kind in ((3, "mixed"), (9, "subnormal"), (20, "nan"), (7, "zeros")):
-        X = _special_x(M, K, 7, kind)
-        b = _special_b(N, 3)
-        _same(h.gemm(X, b), O.base_tcsc(X, t, b))
-        _same(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
+    for M, kind in ((3, "mixed"), (9, "subnormal"), (20, "nan"), (7, "zeros"), (1, "subnormal"), (4, "nan")):
+        for mode in (2, 3):
+            h.set_small_m(mode)
+            X = _special_x(M, K, 7, kind)
+            b = _special_b(N, 3)
+            _same(h.gemm(X, b), O.base_tcsc(X, t, b))
+            _same(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
     h.close()
 
 
@@ -67,7 +82,8 @@ def test_auto_choice_and_structural_edges(tsg, oracle_mod):
     O = oracle_mod
     t = O.tcsc_encode(O.gen_ternary(1024, 4096, 4, 77))
     h = tsg.TCSCDevice(*t.arrays, 1024, 4096)
-    assert h.call_kernel(1) == "tsg_tcsc_ell_kernel" and h.call_kernel(4096) == "tsg_jit_kernel"
+    assert h.call_kernel(1) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(4096) == "tsg_jit_kernel"
+    assert h.call_kernel(2) == "tsg_tcsc_ell_kernel"
     h.set_small_m(1)
     assert h.call_kernel(1) == "tsg_jit_kernel"
     h.close()
@@ -106,7 +122,8 @@ def test_config3_shape_small_m(tsg, oracle_mod, M):
     K, N = 4096, 16384
     arrs = tsg.gen_tcsc(K, N, 4, 42)
     h = tsg.TCSCDevice(*arrs, K, N)
-    assert h.call_kernel(M) == ("tsg_tcsc_ell_kernel" if M <= 64 else "tsg_jit_kernel")
+    assert h.call_kernel(M) == ("tsg_tcsc_ell_pc_kernel" if M == 1 else "tsg_tcsc_ell_kernel" if M <= 64
+                                else "tsg_jit_kernel")
     Xn = O.init_x_frac(M, K, 5)
     b = np.full(N, 2.0, np.float32)
     Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
