@@ -94,6 +94,7 @@ constexpr int kEllAutoMaxM = 64;
 constexpr int kEllAutoMaxMChunked = 16;
 constexpr int kEllTile8 = 2;
 constexpr int kEllMidM = 32;
+constexpr int64_t kEllPcRowsMaxMN = 32768;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
 
 struct DeviceGuard {
@@ -293,6 +294,25 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
     return TSG_OK;
 }
 
+// The producer/consumer walk (tsg_tcsc_ell_pc_kernel) on 1-row tiles when K
+// fits one chunk and the chunk plus its ring fit LDS: few chains, each
+// latency-bound (M = 1: 15.6 vs 20.6 us at K = 4096, N = 16384;
+// profiles/r02x_ell_pc.txt).  TSG_ELL_PC=0 turns it off (diagnostic A/B);
+// tcsc_hip_set_small_m(h, 3) too.
+bool ell_pc_available(const tsg_tcsc *h)
+{
+    static const bool on = [] {
+        const char *e = getenv("TSG_ELL_PC");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || h->small_m == 3 || h->K > tsg::kEllMaxC[0]) return false;
+    const int C = std::min(tsg::kEllMaxC[0], std::max(4, (h->K + 3) / 4 * 4));  // build_ell_image's chunk
+    const size_t lds = tsg::ell_pc_lds_bytes(0, C);
+    return lds > 0 && lds <= tsg::kLdsBytes;
+}
+
+bool use_ell_pc(const tsg_tcsc *h, int v) { return v == 0 && ell_pc_available(h); }
+
 // Small-M kernel choice (DESIGN.md 4 "Small M"): the sliced-ELL walk for a
 // plain-TCSC weight-compiled handle when M is small enough that the jit
 // kernel cannot fill the GPU; -1 = the jit (or rx) kernel.  Measured on
@@ -317,28 +337,16 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     } else {
         while (v + 1 < tsg::kEllVariants && M > tsg::kEllTileM[v]) v++;
     }
+    // M rows as M 1-row producer/consumer tiles while the M index streams stay
+    // small (M = 2 at N = 16384: 20.0 vs 22.9 us; M = 4 at N = 4096: 14.7 vs
+    // 21.9 us; profiles/r02z2_pc_rows.txt)
+    if (M <= 4 && (int64_t)M * h->N <= kEllPcRowsMaxMN && ell_pc_available(h)) v = 0;
     static const int force = [] {  // TSG_ELL_VARIANT: diagnostic sweeps only
         const char *e = getenv("TSG_ELL_VARIANT");
         return e ? atoi(e) : -1;
     }();
     if (force >= 0 && force < tsg::kEllVariants) v = force;
     return v;
-}
-
-// The producer/consumer walk (tsg_tcsc_ell_pc_kernel) for the 1-row tile
-// when K fits one chunk: few chains, each latency-bound (M = 1: 15.6 vs 20.6
-// us at K = 4096, N = 16384; profiles/r02x_ell_pc.txt).  TSG_ELL_PC=0 turns it
-// off (diagnostic A/B).
-bool use_ell_pc(const tsg_tcsc *h, int v)
-{
-    static const bool on = [] {
-        const char *e = getenv("TSG_ELL_PC");
-        return !(e && e[0] == '0');
-    }();
-    if (!on || h->small_m == 3 || v != 0 || h->K > tsg::kEllMaxC[v]) return false;
-    const int C = std::min(tsg::kEllMaxC[v], std::max(4, (h->K + 3) / 4 * 4));  // build_ell_image's chunk
-    const size_t lds = tsg::ell_pc_lds_bytes(v, C);
-    return lds > 0 && lds <= tsg::kLdsBytes;
 }
 
 // Builds and uploads the ELL image of a variant.  Caller holds h->mu.
@@ -776,10 +784,10 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
         if (rc) return rc;
     }
     // the small-M images calls with M <= max_M run: the choice only changes
-    // past an M tile or kEllMidM, so trying M = 1 and each of those + 1
-    // covers them all
-    for (int i = -1; i <= tsg::kEllVariants; i++) {
-        const int m = i < 0 ? 1 : i == tsg::kEllVariants ? kEllMidM + 1 : tsg::kEllTileM[i] + 1;
+    // at M = 1..4 (1-row tiles by M * N), past an M tile or past kEllMidM, so
+    // trying those covers them all
+    for (int i = -4; i <= tsg::kEllVariants; i++) {
+        const int m = i < 0 ? -i : i == tsg::kEllVariants ? kEllMidM + 1 : tsg::kEllTileM[i] + 1;
         const int v = m <= std::max(max_M, 1) ? pick_ell_variant(h, m) : -1;
         if (v >= 0) {
             rc = ensure_ell(h, v);

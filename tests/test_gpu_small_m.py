@@ -16,10 +16,13 @@ pytestmark = pytest.mark.gpu
 SMALL = ("tsg_tcsc_ell_kernel", "tsg_tcsc_ell_pc_kernel")
 
 
-def _small_kernel(M, K, mode):
-    """The kernel tcsc_hip_set_small_m(mode) sends a call with M rows to."""
-    # M = 1 with K within the 1-row tile's LDS chunk (tsg_internal.h kEllMaxC)
-    return "tsg_tcsc_ell_pc_kernel" if mode == 2 and M == 1 and K <= 16380 else "tsg_tcsc_ell_kernel"
+def _small_kernel(M, K, N, mode):
+    """The kernel tcsc_hip_set_small_m(mode) sends a call with M rows to:
+    1-row producer/consumer tiles for M = 1, and for M <= 4 while M * N <=
+    32768, when K fits the 1-row tile's LDS chunk (tsg_capi.cpp
+    pick_ell_variant)."""
+    pc = mode == 2 and K <= 16380 and (M == 1 or (M <= 4 and M * N <= 32768))
+    return "tsg_tcsc_ell_pc_kernel" if pc else "tsg_tcsc_ell_kernel"
 
 
 @pytest.mark.parametrize("mode", [2, 3])
@@ -30,7 +33,7 @@ def test_edges_forced_small_m(tsg, oracle_mod, M, K, N, s, mode):
     t = O.tcsc_encode(W)
     h = tsg.TCSCDevice(*t.arrays, K, N)
     h.set_small_m(mode)
-    assert h.call_kernel(M) == _small_kernel(M, K, mode)
+    assert h.call_kernel(M) == _small_kernel(M, K, N, mode)
     b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
     alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
     for X in (O.init_x_int(M, K, 5), O.init_x_frac(M, K, 6)):
@@ -53,7 +56,7 @@ def test_every_variant_and_tiling(tsg, oracle_mod, M, K, mode):
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, 40 + M))
     h = tsg.TCSCDevice(*t.arrays, K, N)
     h.set_small_m(mode)
-    assert h.call_kernel(M) == _small_kernel(M, K, mode)
+    assert h.call_kernel(M) == _small_kernel(M, K, N, mode)
     b = np.linspace(-3, 3, N).astype(np.float32)
     X = O.init_x_frac(M, K, M)
     assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b)), M
@@ -83,7 +86,7 @@ def test_auto_choice_and_structural_edges(tsg, oracle_mod):
     t = O.tcsc_encode(O.gen_ternary(1024, 4096, 4, 77))
     h = tsg.TCSCDevice(*t.arrays, 1024, 4096)
     assert h.call_kernel(1) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(4096) == "tsg_jit_kernel"
-    assert h.call_kernel(2) == "tsg_tcsc_ell_kernel"
+    assert h.call_kernel(4) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(5) == "tsg_tcsc_ell_kernel"
     h.set_small_m(1)
     assert h.call_kernel(1) == "tsg_jit_kernel"
     h.close()
@@ -112,7 +115,7 @@ def test_auto_choice_and_structural_edges(tsg, oracle_mod):
         hb.set_small_m(2)
 
 
-@pytest.mark.parametrize("M", [1, 16, 32, 64, 96])
+@pytest.mark.parametrize("M", [1, 2, 3, 16, 32, 64, 96])
 def test_config3_shape_small_m(tsg, oracle_mod, M):
     """configs[2]'s K = 4096, N = 16384 at GEMV-like M (the reference sweep's
     M list, plots/run_benchmark.py:8), automatic choice (the small-M kernel up
@@ -122,7 +125,7 @@ def test_config3_shape_small_m(tsg, oracle_mod, M):
     K, N = 4096, 16384
     arrs = tsg.gen_tcsc(K, N, 4, 42)
     h = tsg.TCSCDevice(*arrs, K, N)
-    assert h.call_kernel(M) == ("tsg_tcsc_ell_pc_kernel" if M == 1 else "tsg_tcsc_ell_kernel" if M <= 64
+    assert h.call_kernel(M) == ("tsg_tcsc_ell_pc_kernel" if M <= 2 else "tsg_tcsc_ell_kernel" if M <= 64
                                 else "tsg_jit_kernel")
     Xn = O.init_x_frac(M, K, 5)
     b = np.full(N, 2.0, np.float32)
