@@ -95,6 +95,8 @@ constexpr int kEllAutoMaxMChunked = 16;
 constexpr int kEllTile8 = 2;
 constexpr int kEllMidM = 32;
 constexpr int64_t kEllPcRowsMaxMN = 32768;
+constexpr int kEllStarvedMaxM = 1024;
+constexpr int64_t kEllStarvedWgs = 64;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
 
 struct DeviceGuard {
@@ -321,12 +323,20 @@ bool use_ell_pc(const tsg_tcsc *h, int v) { return v == 0 && ell_pc_available(h)
 // an 8-row chunk of K = 4096 fits LDS, one stream per column); above that the
 // largest tile whose chunk holds K.  Automatic up to M = 64 when an 8-row
 // tile holds K in one chunk (ELL 98 us vs jit 123 us at M = 64, K = 4096),
-// else up to M = 16 (K = 16384: 0.22 vs 0.55 ms).
+// else up to M = 16 (K = 16384: 0.22 vs 0.55 ms); and up to M = 1024 while the
+// jit kernel would have at most 64 workgroups (the reference's (1000, 2048,
+// 512): 31 vs 52 us; (256, 4096, 1024): 34 vs 91 us; at 128 workgroups the
+// jit kernel wins: (1024, 1024, 1024) 32 vs 35 us;
+// profiles/r02_ell_vs_jit_ref.jsonl).
 int pick_ell_variant(const tsg_tcsc *h, int M)
 {
     if (h->kind != tsg_tcsc::kJit || h->B || h->small_m == 1) return -1;
     const bool one8 = h->K <= tsg::kEllMaxC[kEllTile8];
-    if (h->small_m < 2 && M > (one8 ? kEllAutoMaxM : kEllAutoMaxMChunked)) return -1;
+    // the jit kernel's workgroups at its narrowest width (8 columns per wave)
+    const int64_t jit_wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
+                            ((h->N + 8 * tsg::kJitWaves - 1) / (8 * tsg::kJitWaves));
+    const bool starved = M <= kEllStarvedMaxM && jit_wgs <= kEllStarvedWgs;
+    if (h->small_m < 2 && M > (one8 ? kEllAutoMaxM : kEllAutoMaxMChunked) && !starved) return -1;
     int v = 0;
     if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
         v = kEllTile8;

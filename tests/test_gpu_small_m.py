@@ -151,6 +151,25 @@ def test_config0_runs_small_m(tsg, oracle_mod):
     h.close()
 
 
+@pytest.mark.parametrize("M,K,N,small", [(512, 2048, 512, True), (1000, 2048, 512, True), (256, 4096, 1024, True),
+                                         (128, 9000, 1024, True), (1024, 1024, 1024, False), (96, 4096, 16384, False)])
+def test_starved_jit_shapes_take_small_m(tsg, oracle_mod, M, K, N, small):
+    """The reference's cases where the jit kernel would have <= 64 workgroups
+    (plots/run_benchmark.py:8-33) take the small-M kernel automatically up to
+    M = 1024; bit for bit on sampled rows either way."""
+    import torch
+    O = oracle_mod
+    arrs = tsg.gen_tcsc(K, N, 4, 7)
+    h = tsg.TCSCDevice(*arrs, K, N)
+    assert (h.call_kernel(M) in SMALL) == small, h.call_kernel(M)
+    Xn = O.init_x_frac(M, K, 3)
+    b = np.linspace(-1, 1, N).astype(np.float32)
+    Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+    rows = np.unique(np.r_[0, 1, M // 2, M - 1])
+    assert _bits_eq(Y[rows], O.base_tcsc(np.ascontiguousarray(Xn[rows]), O.TCSC(*arrs, K, N), b))
+    h.close()
+
+
 def test_capture_small_m_after_reserve(tsg, oracle_mod):
     import torch
     O = oracle_mod
