@@ -127,12 +127,12 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status);  // legacy default 
 // choice, tsg_ell.hip launch_tcsc_ell), with the K rows per LDS chunk C each
 // allows: (C + 1) * tile floats <= 160 KiB of LDS, float indices C * tile
 // < 65536.  K <= C runs as ONE stream per column (no restaging).
-//   0: M tile 1,  C <= 16380      1: M tile 4,  C <= 10236
+//   0: M tile 1,  C <= 40956      1: M tile 4,  C <= 10236
 //   2: M tile 8,  C <= 5116       3: M tile 16, C <= 2556
 //   4: M tile 32, C <= 1276
 constexpr int kEllVariants = 5;
 constexpr int kEllTileM[kEllVariants] = {1, 4, 8, 16, 32};
-constexpr int kEllMaxC[kEllVariants] = {16380, 10236, 5116, 2556, 1276};
+constexpr int kEllMaxC[kEllVariants] = {40956, 10236, 5116, 2556, 1276};
 struct EllImage {
     int C = 0, nch = 0, steps = 0, nslices = 0;
     std::vector<uint32_t> ent;   // uint16 entries, 2 per word (256-B blocks)

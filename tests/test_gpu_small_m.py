@@ -21,7 +21,9 @@ def _small_kernel(M, K, N, mode):
     1-row producer/consumer tiles for M = 1, and for M <= 4 while M * N <=
     32768, when K fits the 1-row tile's LDS chunk (tsg_capi.cpp
     pick_ell_variant)."""
-    pc = mode == 2 and K <= 16380 and (M == 1 or (M <= 4 and M * N <= 32768))
+    # (the 1-row tile's chunk holds K <= 40956; with the producer/consumer ring
+    # beside it in 160 KiB of LDS, K <= 34812: tsg_ell.hip pc_lds)
+    pc = mode == 2 and K <= 34812 and (M == 1 or (M <= 4 and M * N <= 32768))
     return "tsg_tcsc_ell_pc_kernel" if pc else "tsg_tcsc_ell_kernel"
 
 
@@ -44,13 +46,15 @@ def test_edges_forced_small_m(tsg, oracle_mod, M, K, N, s, mode):
 
 @pytest.mark.parametrize("M,K", [(1, 2300), (2, 2300), (3, 2300), (4, 2300), (5, 2300), (16, 2300), (17, 2300),
                                  (31, 2300), (32, 2300), (33, 2300), (64, 2300), (100, 2300),
-                                 (1, 20000), (1, 16380), (3, 9000), (16, 6000), (40, 6000)])
+                                 (1, 20000), (1, 34812), (1, 34816), (1, 50000), (3, 9000), (16, 6000), (40, 6000)])
 @pytest.mark.parametrize("mode", [2, 3])
 def test_every_variant_and_tiling(tsg, oracle_mod, M, K, mode):
     """M and K pick the M tile (1 / 4 / 8 / 16 / 32 rows) and the lanes per
     column; M past a tile runs several tiles.  K = 2300 fits one LDS chunk for
-    every tile up to 16 rows (one +1/-1 stream per column); K = 6000, 9000 and
-    20000 split into K chunks (a step per pass and chunk, restaged)."""
+    every tile up to 16 rows (one +1/-1 stream per column); K = 6000 and 9000
+    split into K chunks for their tiles (a step per pass and chunk, restaged);
+    M = 1 holds K = 20000 and 34812 in one chunk beside the producer/consumer
+    ring, 34816 without it, 50000 in two chunks."""
     O = oracle_mod
     N = 530
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, 40 + M))
