@@ -132,6 +132,9 @@ int tcsc_hip_reserve(tsg_tcsc *h, int max_M);
  * (BlockedTCSC: 64 only).  Extension: no reference counterpart. */
 int tcsc_hip_jit_width(const tsg_tcsc *h, int M);
 int tcsc_hip_set_jit_width(tsg_tcsc *h, int width);
+/* Waves per workgroup of that call's image: 8, or 4 (narrow widths at mid M:
+ * twice the workgroups of the same width). */
+int tcsc_hip_jit_waves(const tsg_tcsc *h, int M);
 
 /* Small-M kernel (no reference counterpart; DESIGN.md 4 "Small M"): calls
  * with few rows (GEMV-like: M <= 64 when K fits an 8-row LDS chunk, else
@@ -234,6 +237,12 @@ int tsg_jit_codegen_w(const int32_t *col_start_pos, const int32_t *col_start_neg
                       const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
                       int B, int width, uint32_t *code, int64_t code_cap, int64_t *code_len,
                       uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+
+/* ... and waves per workgroup (8; 4 for widths 32, 16, 8: the mid-M shapes). */
+int tsg_jit_codegen_wv(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                       const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                       int B, int width, int waves, uint32_t *code, int64_t code_cap, int64_t *code_len,
+                       uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
 
 /* Checks BlockedTCSC<B> arrays (layout as tcsc_hip_create_blocked): monotone
  * column starts, every row inside its block, ascending, no row both +1 and -1. */

@@ -75,8 +75,9 @@ def main():
                           "kernel_ms": round(ms, 4), "step_ms": round(step_ms, 4),
                           "gflops_kernel": round(adds / (ms * 1e-3) / 1e9, 1),
                           "valu_frac": round(adds / (ms * 1e-3) / 78.64e12, 4),
-                          "jit_width": jw, "width_pinned": bool(width),
-                          "workgroups": -(-M // 128) * -(-N // (8 * max(jw, 1))), "register_s": round(reg_s, 2),
+                          "jit_width": jw, "jit_waves": h.jit_waves(M), "width_pinned": bool(width),
+                          "workgroups": -(-M // 128) * -(-N // (h.jit_waves(M) * max(jw, 1))),
+                          "register_s": round(reg_s, 2),
                           "bit_identical_rows": ok}), flush=True)
         h.close()
 

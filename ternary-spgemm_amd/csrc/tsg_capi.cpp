@@ -38,16 +38,16 @@ struct tsg_tcsc {
     // TSG_KERNEL=rx)
     enum Kind { kRx, kJit } kind = kJit;
     tsg::RxImage rimg;                    // device image of the rx kernel
-    // jit kernel: one compiled image per stream width (index tsg::kJitWidths):
-    // the default width at registration, narrower ones on the first call with
-    // an M that picks them (or tcsc_hip_reserve)
+    // jit kernel: one compiled image per (stream width, waves per workgroup)
+    // (shape_index): the default shape at registration, others on the first
+    // call with an M that picks them (or tcsc_hip_reserve)
     struct JitVariant {
-        int nw = 0, Npad = 0;
+        int nw = 0, waves = 0, Npad = 0;
         tsg::JitModule mod;               // dispatcher + generated code, loaded
         uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
         int64_t code_bytes = 0, wcode_words = 0;
     };
-    JitVariant jv[4];
+    JitVariant jv[7];
     int jit_nch = 0;                      // X^T chunks (all widths)
     int jit_force = 0;                    // tcsc_hip_set_jit_width / TSG_JIT_NW: 0 = auto
     uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
@@ -96,6 +96,7 @@ constexpr int kEllTile8 = 2;
 constexpr int kEllMidM = 32;
 constexpr int64_t kEllPcRowsMaxMN = 32768;
 constexpr int kEllStarvedMaxM = 1024;
+constexpr int64_t kJitFullWgs = 230;
 constexpr int64_t kEllStarvedWgs = 64;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
 
@@ -191,59 +192,86 @@ int width_index(int nw)
     return -1;
 }
 
-// Stream width for a call with M rows (DESIGN.md 4 "Small M").  A workgroup is
-// one 128-row M tile x 8 streams of nw columns; it walks every X^T chunk once
-// per pass.  Per step and workgroup the adds cost 8 * nw * 96 * d * 4 / 4
-// VALU cycles at ~65% issue efficiency (d: nonzeros per pass per entry) and
-// the X-row reads 8 * 96 * (1 - (1 - d)^nw) * 512 B of LDS at 128 B/clk; a
-// launch is ceil(workgroups / 256 CUs) rounds of 2 * nch steps.  Narrow
-// streams win when the default width leaves CUs idle (config 2: 32 of 256).
-int pick_jit_width(const tsg_tcsc *h, int M)
+// jv index of a (width, waves) shape: 8-wave widths 0..3, 4-wave widths 32/16/8 4..6
+int shape_index(int nw, int waves)
 {
-    if (h->B) return tsg::kJitNW;
-    if (h->jit_force) return h->jit_force;
-    const double KN = std::max(1.0, (double)h->K * (double)h->N);
-    const double mt = (double)((std::max(M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM);
-    int best = tsg::kJitNW;
-    double best_t = 0;
-    for (int nw : tsg::kJitWidths) {
-        if (!tsg::jit_width_ok(nw)) continue;
-        const double ntile = (double)((h->N + 8 * nw - 1) / (8 * nw)), tiles = mt * ntile;
-        const double rounds = std::ceil(tiles / 256.0);
-        double t = 0, image = 8.0 * (double)(h->nnz_pos + h->nnz_neg);
-        for (const int64_t nnz : {h->nnz_pos, h->nnz_neg}) {
-            const double d = (double)nnz / KN, rows = tsg::kJitChunk * (1.0 - std::pow(1.0 - d, nw));
-            const double valu = 8.0 * nw * tsg::kJitChunk * d / 0.65;
-            const double lds = 8.0 * rows * 512.0 / 128.0;
-            t += (std::max(valu, lds) + 300.0) * h->jit_nch;
-            image += ntile * 8.0 * h->jit_nch * (160.0 + 8.0 * rows);  // reads + step scaffolding
-        }
-        t *= rounds;
-        if (nw != tsg::kJitNW && image > 2.0 * (double)(1ull << 30)) continue;  // 32-bit stream offsets
-        if (best_t == 0 || t < 0.97 * best_t) {
-            best = nw;
-            best_t = t;
-        }
-    }
-    return best;
+    const int w = width_index(nw);
+    if (w < 0 || !tsg::jit_waves_ok(nw, waves)) return -1;
+    return waves == tsg::kJitWaves ? w : 3 + w;
 }
 
-// Compiles and loads the image of one stream width (registration, or the first
-// call that picks the width).  Caller holds h->mu (or owns h exclusively).
-int ensure_jit_variant(tsg_tcsc *h, int nw)
+struct JitShape {
+    int nw, waves;
+};
+
+// Shape (stream width x waves per workgroup) for a call with M rows.  Every
+// shape walks the same X^T chunks; a wider stream reads fewer LDS bytes per
+// add (32 / width: an X pair read feeds width x 2 rows x d adds), and a
+// workgroup needs a CU.  Rule (measured, profiles/r02w4_waves_ab.txt,
+// r02_ref_cases.jsonl): the widest stream among the shapes that still give
+// >= 230 workgroups (~90% of the CUs: (16000, 1024, 1024) runs 64 x 8 on 250,
+// 0.116 ms, not 32 x 8 on 500, 0.141 ms), 8 waves before 4 at equal width;
+// if none does, the most workgroups.  configs[1]
+// (M = 512, N = 4096): 16 columns x 4 waves, 0.105 ms (8 x 8: 0.120);
+// M = 256, N = 16384: 32 x 4, 0.153 ms (16 x 8: 0.173); M >= 1024: 64 x 8.
+// A pinned width (tcsc_hip_set_jit_width) runs 8 waves; TSG_JIT_WAVES=4 forces
+// 4 waves for every narrow width (diagnostic).
+JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 {
-    const int i = width_index(nw);
-    if (i < 0 || !tsg::jit_width_ok(nw)) return fail(TSG_ERR_ARG, "unsupported jit stream width " + std::to_string(nw));
+    static const int env_waves = [] {
+        const char *e = getenv("TSG_JIT_WAVES");
+        return e ? atoi(e) : 0;
+    }();
+    if (h->B) return {tsg::kJitNW, tsg::kJitWaves};
+    if (h->jit_force) {
+        const int w = env_waves == 4 && tsg::jit_waves_ok(h->jit_force, 4) ? 4 : tsg::kJitWaves;
+        return {h->jit_force, w};
+    }
+    const int64_t mt = (std::max(M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM;
+    const double image8 = 8.0 * (double)(h->nnz_pos + h->nnz_neg);
+    JitShape best{tsg::kJitNW, tsg::kJitWaves}, most{tsg::kJitNW, tsg::kJitWaves};
+    int64_t most_wgs = -1;
+    bool full = false;
+    for (int nw : tsg::kJitWidths) {
+        for (int waves : {tsg::kJitWaves, 4}) {
+            if (!tsg::jit_waves_ok(nw, waves)) continue;
+            if (env_waves == 4 && nw != tsg::kJitNW && waves != 4) continue;
+            const int64_t ntile = (h->N + (int64_t)waves * nw - 1) / ((int64_t)waves * nw), wgs = mt * ntile;
+            // narrow streams repeat the reads and step scaffolding per stream:
+            // keep the image inside the 32-bit stream offsets
+            const double image = image8 + (double)ntile * waves * h->jit_nch * 2 * (160.0 + 8.0 * tsg::kJitChunk);
+            if (nw != tsg::kJitNW && image > 2.0 * (double)(1ull << 30)) continue;
+            if (!full && wgs >= kJitFullWgs) {  // widths come widest first
+                best = {nw, waves};
+                full = true;
+            }
+            if (wgs > most_wgs) {
+                most_wgs = wgs;
+                most = {nw, waves};
+            }
+        }
+    }
+    return full ? best : most;
+}
+
+// Compiles and loads the image of one shape (registration, or the first call
+// that picks it).  Caller holds h->mu (or owns h exclusively).
+int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves)
+{
+    const int i = shape_index(nw, waves);
+    if (i < 0 || !tsg::jit_width_ok(nw))
+        return fail(TSG_ERR_ARG, "unsupported jit stream width " + std::to_string(nw) + " x " + std::to_string(waves) +
+                                 " waves");
     tsg_tcsc::JitVariant &v = h->jv[i];
     if (v.mod.function) return TSG_OK;
     tsg::JitImage img;
     tsg::build_jit_code(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
-                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw);
+                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw, waves);
     // stream offsets (wcode) and the dispatcher's region literal are 32-bit
     if ((uint64_t)img.code.size() * 4 >= (1ull << 32) - (1ull << 20))
         return fail(TSG_ERR_RANGE, "jit image of " + std::to_string((uint64_t)img.code.size() * 4) +
                                        " B exceeds the 32-bit stream offsets; shard W's columns");
-    if (nw == tsg::kJitNW)
+    if (nw == tsg::kJitNW && waves == tsg::kJitWaves)
         if (const char *d = std::getenv("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
             const size_t S = tsg::kJitStreams;
             if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
@@ -254,7 +282,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
                 for (size_t k = 0; k < img.wcode.size(); k++) img.wcode[k] = img.wcode[k & ~(size_t)1];
         }
     DeviceGuard g(h->device);
-    const std::string err = v.mod.load(img.code, nw);
+    const std::string err = v.mod.load(img.code, nw, waves);
     if (!err.empty()) return fail(TSG_ERR_HIP, "jit kernel (width " + std::to_string(nw) + "): " + err);
     const size_t wb = img.wcode.size() * sizeof(uint32_t);
     if (hipMalloc(&v.d_wcode, std::max<size_t>(wb, 4)) != hipSuccess) {
@@ -289,6 +317,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw)
                                  "generated code region (status " + std::to_string(st[0]) + ")");
     }
     v.nw = nw;
+    v.waves = waves;
     v.Npad = img.Npad;
     v.code_bytes = (int64_t)img.code.size() * 4;
     v.wcode_words = (int64_t)img.wcode.size();
@@ -435,17 +464,17 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     dims_for(h, M, Mp, Kp);
     tsg_tcsc::JitVariant *jv = nullptr;
     if (h->kind == tsg_tcsc::kJit) {
-        const int nw = pick_jit_width(h, M);
-        jv = &h->jv[width_index(nw)];
+        const JitShape sh = pick_jit_shape(h, M);
+        jv = &h->jv[shape_index(sh.nw, sh.waves)];
         if (!jv->mod.function && capturing)
-            return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(nw) +
+            return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(sh.nw) +
                                          " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
-        rc = ensure_jit_variant(h, nw);
+        rc = ensure_jit_variant(h, sh.nw, sh.waves);
         if (rc) return rc;
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
-        const int64_t wgs = (int64_t)(Mp / tsg::kJitTileM) * (jv->Npad / (jv->nw * tsg::kJitStreams));
-        if ((int64_t)Mp * tsg::kJitChunk * 4 >= (1ll << 31) || wgs * tsg::kJitWaves * 64 >= (1ll << 32))
+        const int64_t wgs = (int64_t)(Mp / tsg::kJitTileM) * (jv->Npad / (jv->nw * jv->waves));
+        if ((int64_t)Mp * tsg::kJitChunk * 4 >= (1ll << 31) || wgs * jv->waves * 64 >= (1ll << 32))
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " is too large for one jit launch; split the rows");
     }
     // X^T of the previous call may still be read by its kernel on another
@@ -467,7 +496,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
-                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * tsg::kJitStreams, s)
+                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves, jv->waves, s)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)
@@ -775,7 +804,7 @@ extern "C" int tcsc_hip_create_csc_packed(const int32_t *col_ptr, const int32_t 
 extern "C" void tcsc_hip_destroy(tsg_tcsc *h) { free_handle(h); }
 
 // Prepares every call with M <= max_M: the work buffer for max_M rows and the
-// image of every stream width such a call picks (pick_jit_width depends on M
+// image of every shape such a call picks (pick_jit_shape depends on M
 // only through the number of 128-row M tiles).  After it, calls with M <=
 // max_M allocate and compile nothing, so they can be captured in a graph.
 extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
@@ -790,7 +819,8 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
         const int m = std::min(max_M, mt * tsg::kJitTileM);
         if (pick_ell_variant(h, m) >= 0 && pick_ell_variant(h, std::min(m, (mt - 1) * tsg::kJitTileM + 1)) >= 0)
             continue;  // every M of this tile runs the small-M kernel
-        rc = ensure_jit_variant(h, pick_jit_width(h, m));
+        const JitShape sh = pick_jit_shape(h, m);
+        rc = ensure_jit_variant(h, sh.nw, sh.waves);
         if (rc) return rc;
     }
     // the small-M images calls with M <= max_M run: the choice only changes
@@ -821,7 +851,13 @@ extern "C" int tcsc_hip_set_jit_width(tsg_tcsc *h, int width)
 extern "C" int tcsc_hip_jit_width(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
-    return pick_jit_width(h, M);
+    return pick_jit_shape(h, M).nw;
+}
+
+extern "C" int tcsc_hip_jit_waves(const tsg_tcsc *h, int M)
+{
+    if (!h || h->kind != tsg_tcsc::kJit) return 0;
+    return pick_jit_shape(h, M).waves;
 }
 
 extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)

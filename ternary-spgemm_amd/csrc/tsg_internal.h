@@ -97,27 +97,32 @@ constexpr uint32_t kJitFormat = 2;                      // region header word 7 
 // (tsg_capi.cpp pick_jit_width).  BlockedTCSC runs at kJitNW only.
 constexpr int kJitWidths[] = {kJitNW, 32, 16, 8};
 inline bool jit_width_ok(int nw) { return nw == kJitNW || nw == 32 || nw == 16 || nw == 8; }
+// waves per workgroup: 8, or 4 for the narrow widths (lib/tsg_jit_w<nw>_4w.co):
+// the same 48 KiB chunks staged by 4 waves (12 DMA pieces each), half the
+// columns per workgroup -> twice the workgroups at mid M
+inline bool jit_waves_ok(int nw, int waves) { return waves == kJitWaves || (waves == 4 && nw != kJitNW); }
 
 struct JitImage {
-    int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0;
+    int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0, waves = kJitWaves;
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
     std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
 };
 // B = 0: BaseTCSC order (comp.h:25-69); B > 0: BaseBlockedTCSC<B> order
 // (comp.h:607-658) from BlockedTCSC<B> arrays
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
-                    const int32_t *rin, int K, int N, int B, JitImage &img, int nw = kJitNW);
+                    const int32_t *rin, int K, int N, int B, JitImage &img, int nw = kJitNW,
+                    int waves = kJitWaves);
 
 struct JitModule {
     void *module = nullptr;        // hipModule_t
     void *function = nullptr;      // hipFunction_t of tsg_jit_kernel
     void *probe = nullptr;         // hipFunction_t of tsg_jit_probe (region check, at load)
-    std::string load(const std::vector<uint32_t> &code, int nw = kJitNW);  // "" on success
+    std::string load(const std::vector<uint32_t> &code, int nw = kJitNW, int waves = kJitWaves);  // "" on success
     void unload();
 };
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
-                    int prelu, uint32_t *status, int tile_cols, void *stream);
+                    int prelu, uint32_t *status, int tile_cols, int waves, void *stream);
 int launch_jit_probe(const JitModule &jm, uint32_t *status);  // legacy default stream
 
 // ---------------------------------------------------------------------------

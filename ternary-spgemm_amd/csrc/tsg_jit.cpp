@@ -120,16 +120,25 @@ struct Emit {
 // accumulators from the next even register.
 constexpr uint32_t kPairBytes = kJitTileM * 8;            // one k-row pair of the tile in LDS: 1 KiB
 constexpr uint32_t kBufBytes = kJitChunk / 2 * kPairBytes; // one LDS chunk buffer (48 KiB)
-constexpr int kPieces = kJitChunk / 2 / kJitWaves;        // DMA pieces (pair rows) per wave per chunk
-static_assert(kPieces * kJitWaves * 2 == kJitChunk, "chunk pairs split in pieces over the waves");
 static_assert(kPairBytes == 1024, "one LDS-DMA piece (64 lanes x 16 B) is one pair row");
 constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 4s : 11 + 4s]
 constexpr uint32_t kLdsBaseV = kXSlot0 + kJitXRegs;        // + b: buffer b + lane * 16
 constexpr uint32_t kSinkV = kLdsBaseV + kJitRing;
 constexpr uint32_t kDmaOffV = kSinkV + 1;                  // + i: DMA piece i offsets
-constexpr uint32_t kLane128V = kDmaOffV + kPieces;
-constexpr uint32_t kAcc0 = (kLane128V + 2) & ~1u;         // column c: v[acc0 + 2c : acc0 + 2c + 1]
-static_assert(kAcc0 + 2 * kJitNW <= 256u, "VGPR budget");
+// then, by the waves W of the workgroup: chunk/2/W DMA piece offsets, lane*128,
+// and the accumulators from the next even register (JitRegs)
+struct JitRegs {
+    int pieces;         // DMA pieces (pair rows) per wave per chunk
+    uint32_t lane128;   // v[lane * 128]
+    uint32_t acc0;      // column c: v[acc0 + 2c : acc0 + 2c + 1]
+    explicit JitRegs(int waves)
+        : pieces(kJitChunk / 2 / waves), lane128(kDmaOffV + (uint32_t)(kJitChunk / 2 / waves)),
+          acc0((kDmaOffV + (uint32_t)(kJitChunk / 2 / waves) + 2) & ~1u)
+    {
+    }
+};
+static_assert(((kDmaOffV + kJitChunk / 2 / kJitWaves + 2) & ~1u) + 2 * kJitNW <= 256u, "VGPR budget");
+static_assert(((kDmaOffV + kJitChunk / 2 / 4 + 2) & ~1u) + 2 * 32 <= 256u, "VGPR budget, 4 waves");
 // narrower streams (jit width < kJitNW) use the same register contract, fewer accumulators
 constexpr int kTailPad = 32768 + 1024;   // words of padding after the last stream (code prefetch reads ahead)
 static_assert((kJitChunk / 2 - 1) * kPairBytes + 8 < 65536, "ds_read offset field");
@@ -189,14 +198,20 @@ std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw)
 }  // namespace
 
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
-                    int K, int N, int B, JitImage &img, int nw)
+                    int K, int N, int B, JitImage &img, int nw, int waves)
 {
     if (nw <= 0) nw = kJitNW;
-    const int tile_cols = nw * kJitStreams;
+    if (!jit_waves_ok(nw, waves)) waves = kJitWaves;
+    const JitRegs R(waves);
+    const int streams = waves;  // one stream per wave (no M split)
+    const int kPieces = R.pieces;
+    const uint32_t kLane128V = R.lane128, kAcc0 = R.acc0;
+    const int tile_cols = nw * streams;
     img.K = K;
     img.N = N;
     img.B = B;
     img.nw = nw;
+    img.waves = waves;
     img.Npad = ((N + tile_cols - 1) / tile_cols) * tile_cols;
     img.nch = std::max(1, (K + kJitChunk - 1) / kJitChunk);
     const int nch = img.nch, ntiles = img.Npad / tile_cols;
@@ -206,19 +221,19 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // columns (nw registers) at the top of that range
     const int S = B ? (kJitXRegs - nw) / kJitSlotRegs : kJitSlots;
     const uint32_t kTmp0 = kXSlot0 + (uint32_t)(kJitSlotRegs * S);  // y of column c0 + c: v[tmp0 + 2c : +1]
-    img.wcode.assign((size_t)ntiles * kJitStreams, 0u);
+    img.wcode.assign((size_t)ntiles * streams, 0u);
     std::vector<uint32_t> &code = img.code;
     code.clear();
     const int64_t slots = (B ? (int64_t)(K / B) : 1) * N;
     const int64_t nnz = (int64_t)csp[slots] + (int64_t)csn[slots];
-    code.reserve((size_t)nnz * 2 + (size_t)ntiles * kJitStreams * ((size_t)steps * 150 + 64) + kTailPad + 64);
+    code.reserve((size_t)nnz * 2 + (size_t)ntiles * streams * ((size_t)steps * 150 + 64) + kTailPad + 64);
     // header: magic, then the geometry (tests/test_jit_codegen.py derives the
     // register contract from it), the block size, the X slots in use, the
     // ring and the X^T layout
     code.insert(code.end(), {kJitMagic0, kJitMagic1,
-                             (uint32_t)kJitWaves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
+                             (uint32_t)waves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
-                             (uint32_t)kJitStreams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
+                             (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
                              (uint32_t)kJitRing | kJitFormat << 8});
     Emit E{code, std::getenv("TSG_JIT_NOALIGN") == nullptr};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
@@ -313,9 +328,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         return kXSlot0 + (uint32_t)(kJitSlotRegs * (g % S)) + (rd.mask == 3 ? 2u * (uint32_t)half : 0u);
     };
     for (int t = 0; t < ntiles; t++) {
-        for (int w = 0; w < kJitStreams; w++) {
+        for (int w = 0; w < streams; w++) {
             while (code.size() % 64) E.nop();  // 256-B aligned stream start
-            img.wcode[(size_t)t * kJitStreams + w] = E.pos_bytes();
+            img.wcode[(size_t)t * streams + w] = E.pos_bytes();
             n0 = t * tile_cols + w * nw;
             std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
@@ -429,10 +444,12 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
 namespace {
 
 // The dispatcher of a stream width: lib/tsg_jit.co (kJitNW columns per wave)
-// or lib/tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile).
-std::string template_path(int nw)
+// or lib/tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile);
+// 4-wave workgroups: lib/tsg_jit_w<nw>_4w.co (TSG_JIT_WAVES=4).
+std::string template_path(int nw, int waves)
 {
-    const std::string name = nw == kJitNW ? "tsg_jit.co" : "tsg_jit_w" + std::to_string(nw) + ".co";
+    const std::string name = nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
+                             : "tsg_jit_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co";
     if (const char *dir = std::getenv("TSG_JIT_DIR")) return std::string(dir) + "/" + name;  // tests: rx fallback
     Dl_info info;
     if (dladdr(reinterpret_cast<void *>(&build_jit_code), &info) && info.dli_fname) {
@@ -445,9 +462,9 @@ std::string template_path(int nw)
 
 }  // namespace
 
-std::string JitModule::load(const std::vector<uint32_t> &code, int nw)
+std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves)
 {
-    const std::string path = template_path(nw);
+    const std::string path = template_path(nw, waves);
     std::ifstream f(path, std::ios::binary);
     if (!f) return "cannot open jit template " + path;
     std::vector<unsigned char> img((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -536,14 +553,14 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status)
 
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
-                    uint32_t *status, int tile_cols, void *stream)
+                    uint32_t *status, int tile_cols, int waves, void *stream)
 {
     int mtiles = Mp / kJitTileM, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
                       (void *)&status};
     hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.function, (unsigned)(mtiles * ntiles), 1, 1,
-                                         kJitWaves * 64, 1, 1, 0, (hipStream_t)stream, params, nullptr);
+                                         (unsigned)waves * 64u, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;
 }
 
@@ -552,10 +569,15 @@ int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t
 // ---------------------------------------------------------------- C-ABI --
 extern thread_local std::string g_tsg_host_err;
 
-extern "C" int tsg_jit_codegen_w(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
-                                 int K, int N, int B, int width, uint32_t *code, int64_t code_cap,
-                                 int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
+extern "C" int tsg_jit_codegen_wv(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                                  int K, int N, int B, int width, int waves, uint32_t *code, int64_t code_cap,
+                                  int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
 {
+    if (!tsg::jit_waves_ok(width, waves)) {
+        g_tsg_host_err = "tsg_jit_codegen: unsupported waves per workgroup " + std::to_string(waves) +
+                         " for width " + std::to_string(width) + " (8; 4 for widths 32, 16, 8)";
+        return TSG_ERR_ARG;
+    }
     if (!tsg::jit_width_ok(width) || (B && width != tsg::kJitNW)) {
         g_tsg_host_err = "tsg_jit_codegen: unsupported stream width " + std::to_string(width) +
                          (B ? " for BlockedTCSC (64 only)" : " (64, 32, 16 or 8)");
@@ -571,7 +593,7 @@ extern "C" int tsg_jit_codegen_w(const int32_t *csp, const int32_t *csn, const i
         return TSG_ERR_ARG;
     }
     tsg::JitImage img;
-    tsg::build_jit_code(csp, csn, rip, rin, K, N, B, img, width);
+    tsg::build_jit_code(csp, csn, rip, rin, K, N, B, img, width, waves);
     if (code_len) *code_len = (int64_t)img.code.size();
     if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
     if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
@@ -581,6 +603,14 @@ extern "C" int tsg_jit_codegen_w(const int32_t *csp, const int32_t *csn, const i
     if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);
     if (wcode) std::memcpy(wcode, img.wcode.data(), img.wcode.size() * 4);
     return TSG_OK;
+}
+
+extern "C" int tsg_jit_codegen_w(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                                 int K, int N, int B, int width, uint32_t *code, int64_t code_cap,
+                                 int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
+{
+    return tsg_jit_codegen_wv(csp, csn, rip, rin, K, N, B, width, tsg::kJitWaves, code, code_cap, code_len, wcode,
+                              wcode_cap, wcode_len);
 }
 
 extern "C" int tsg_jit_codegen_blocked(const int32_t *csp, const int32_t *csn, const int32_t *rip,

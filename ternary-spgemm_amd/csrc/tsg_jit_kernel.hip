@@ -26,7 +26,8 @@
 // p = 0 the +1 entries, p = 1 the -1 entries), X pairs read with ds_read_b128
 // (both k rows at once), the next step's first reads issued before the
 // barrier, the stream's own code touched ahead (L2 prefetch).
-// Register contract (tsg_jit.cpp):
+// Register contract (tsg_jit.cpp), 8 waves (4 waves: 12 pieces v108-119,
+// lane*128 v120, accumulators from v122):
 //   v[8:104)   24 X slots of 4 VGPRs (k-row pair: row 2p in v[s:s+1], 2p+1 in v[s+2:s+3])
 //   v104-106   LDS byte address of lane*16 in ring buffer 0..2
 //   v107       code-prefetch sink
@@ -43,14 +44,21 @@
 
 namespace {
 
-constexpr int kJWaves = 8;
 // TSG_JIT_NW: a narrower stream width (32, 16 or 8 columns per wave;
-// lib/tsg_jit_w<NW>.co) -- more workgroups for small M, same registers
+// lib/tsg_jit_w<NW>.co) -- more workgroups for small M, same registers.
+// TSG_JIT_WAVES=4 (narrow widths, lib/tsg_jit_w<NW>_4w.co): 4-wave workgroups,
+// twice the workgroups again; each wave stages 12 of the chunk's 48 pair
+// rows, so the piece offsets take v108-119, lane*128 v120, accumulators from v122.
 #ifndef TSG_JIT_NW
 #define TSG_JIT_NW 64
 #endif
+#ifndef TSG_JIT_WAVES
+#define TSG_JIT_WAVES 8
+#endif
+constexpr int kJWaves = TSG_JIT_WAVES;
 constexpr int kJNW = TSG_JIT_NW;
 static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8, "stream width");
+static_assert(kJWaves == 8 || (kJWaves == 4 && kJNW < 64), "waves per workgroup");
 constexpr int kJTileM = 128;
 constexpr int kJTileCols = kJWaves * kJNW;
 constexpr int kJRing = 3;                            // LDS buffers in the X^T ring (tsg_internal.h)
@@ -62,9 +70,17 @@ constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region head
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 typedef float F32x16 __attribute__((ext_vector_type(16)));
 
+#if TSG_JIT_WAVES == 8
 #define TSG_JIT_IN                                                                                  \
     "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),             \
         "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+#else
+#define TSG_JIT_IN                                                                                  \
+    "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),             \
+        "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(off[6]), \
+        "{v115}"(off[7]), "{v116}"(off[8]), "{v117}"(off[9]), "{v118}"(off[10]), "{v119}"(off[11]), \
+        "{v120}"(l128)
+#endif
 
 #define TSG_JIT_CLOBBERS \
     "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", \
@@ -180,24 +196,36 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb), \
                    TSG_JIT_IN                                                                       \
                  : TSG_JIT_CLOBBERS)
-#if TSG_JIT_NW == 64
+#if TSG_JIT_WAVES == 8 && TSG_JIT_NW == 64
     F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
     TSG_JIT_CALL("+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3));
     auto acc_of = [&](int c, int r) {
         return c < 16 ? a0[2 * (c & 15) + r] : c < 32 ? a1[2 * (c & 15) + r]
              : c < 48 ? a2[2 * (c & 15) + r] : a3[2 * (c & 15) + r];
     };
-#elif TSG_JIT_NW == 32
+#elif TSG_JIT_WAVES == 8 && TSG_JIT_NW == 32
     F32x32 a0 = {}, a1 = {};  // comp.h:41
     TSG_JIT_CALL("+{v[116:147]}"(a0), "+{v[148:179]}"(a1));
     auto acc_of = [&](int c, int r) { return c < 16 ? a0[2 * (c & 15) + r] : a1[2 * (c & 15) + r]; };
-#elif TSG_JIT_NW == 16
+#elif TSG_JIT_WAVES == 8 && TSG_JIT_NW == 16
     F32x32 a0 = {};  // comp.h:41
     TSG_JIT_CALL("+{v[116:147]}"(a0));
     auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
-#else
+#elif TSG_JIT_WAVES == 8
     F32x16 a0 = {};  // comp.h:41
     TSG_JIT_CALL("+{v[116:131]}"(a0));
+    auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
+#elif TSG_JIT_NW == 32  // 4 waves: accumulators from v122
+    F32x32 a0 = {}, a1 = {};  // comp.h:41
+    TSG_JIT_CALL("+{v[122:153]}"(a0), "+{v[154:185]}"(a1));
+    auto acc_of = [&](int c, int r) { return c < 16 ? a0[2 * (c & 15) + r] : a1[2 * (c & 15) + r]; };
+#elif TSG_JIT_NW == 16
+    F32x32 a0 = {};  // comp.h:41
+    TSG_JIT_CALL("+{v[122:153]}"(a0));
+    auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
+#else
+    F32x16 a0 = {};  // comp.h:41
+    TSG_JIT_CALL("+{v[122:137]}"(a0));
     auto acc_of = [&](int c, int r) { return a0[2 * c + r]; };
 #endif
 #undef TSG_JIT_CALL

@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "tsg_gen_tcsc", "tsg_gen_x", "tcsc_hip_create_csc_packed", "tsg_tcsc_to_csc_packed",
     "tsg_csc_packed_to_tcsc", "tsg_jit_codegen", "tcsc_hip_kernel_name", "tcsc_hip_encode_dense_dev",
     "tcsc_hip_create_blocked", "tsg_jit_codegen_blocked", "tsg_blocked_tcsc_validate",
-    "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tsg_jit_codegen_w",
+    "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tcsc_hip_jit_waves", "tsg_jit_codegen_w", "tsg_jit_codegen_wv",
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build",
 )
 
@@ -121,12 +121,15 @@ def lib() -> C.CDLL:
                                           C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tsg_jit_codegen_w.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                     C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
+    L.tsg_jit_codegen_wv.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
+                                     C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tcsc_hip_set_small_m.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.restype = C.c_char_p
     L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
                                 vp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     L.tcsc_hip_jit_width.argtypes = [H, C.c_int]
+    L.tcsc_hip_jit_waves.argtypes = [H, C.c_int]
     L.tcsc_hip_set_jit_width.argtypes = [H, C.c_int]
     for f in EXPORTED_SYMBOLS:
         if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name", "tcsc_hip_call_kernel"):
@@ -223,20 +226,21 @@ def csc_packed_to_tcsc(col_ptr, row_idx, packed, N: int):
     return o[0], o[1], o[2][: p.value], o[3][: q.value]
 
 
-def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0, width: int = 64):
+def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0, width: int = 64, waves: int = 8):
     """Host-side machine code of the weight-compiled kernel (TSG_KERNEL=jit):
     (region words uint32[], per-(tile, wave) stream byte offsets uint32[]).
     B > 0: the arrays are BlockedTCSC<B> (tcsc_hip_create_blocked); width:
-    columns per stream (64, 32, 16, 8)."""
+    columns per stream (64, 32, 16, 8); waves per workgroup (8; 4 for the
+    narrow widths)."""
     csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
     nc, nw = C.c_int64(), C.c_int64()
     L = lib()
-    _check(L.tsg_jit_codegen_w(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B, width, None, 0,
-                               C.byref(nc), None, 0, C.byref(nw)), "tsg_jit_codegen")
+    _check(L.tsg_jit_codegen_wv(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B, width, waves, None, 0,
+                                C.byref(nc), None, 0, C.byref(nw)), "tsg_jit_codegen")
     code = np.empty(nc.value, np.uint32)
     wcode = np.empty(nw.value, np.uint32)
-    _check(L.tsg_jit_codegen_w(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B, width, _ptr(code),
-                               nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
+    _check(L.tsg_jit_codegen_wv(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B, width, waves, _ptr(code),
+                                nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
            "tsg_jit_codegen")
     return code, wcode
 
@@ -492,6 +496,10 @@ class TCSCDevice:
     def jit_width(self, M: int) -> int:
         """Columns per stream a call with M rows runs (0: not the jit kernel)."""
         return int(lib().tcsc_hip_jit_width(self._h, M))
+
+    def jit_waves(self, M: int) -> int:
+        """Waves per workgroup of that call's jit image (8, or 4 at mid M)."""
+        return int(lib().tcsc_hip_jit_waves(self._h, M))
 
     def set_jit_width(self, width: int) -> None:
         """0 = automatic per call (default); 64/32/16/8 pins the stream width."""

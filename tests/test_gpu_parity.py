@@ -128,6 +128,31 @@ def test_auto_width_small_m(tsg, oracle_mod):
     h.close()
 
 
+@pytest.mark.parametrize("M,K,N,shape", [(512, 4096, 4096, (16, 4)), (256, 2048, 16384, (32, 4)),
+                                         (1024, 1024, 4096, (32, 4)), (4096, 1024, 16384, (64, 8)),
+                                         (300, 1000, 700, None)])
+def test_auto_shape_mid_m(tsg, oracle_mod, M, K, N, shape):
+    """The automatic (width, waves) shape at mid M: 4-wave workgroups where
+    they double the workgroups of a wider stream (configs[1] takes 16 x 4);
+    every launched shape bit for bit on sampled rows, and one handle switching
+    shapes call by call."""
+    import torch
+    O = oracle_mod
+    arrs = tsg.gen_tcsc(K, N, 4, 5)
+    h = tsg.TCSCDevice(*arrs, K, N)
+    h.set_small_m(1)
+    if shape is not None:
+        assert (h.jit_width(M), h.jit_waves(M)) == shape
+    b = torch.linspace(-2, 2, N, device="cuda")
+    for m in (M, 128 * 12 + 3, M // 2 + 1):
+        Xn = O.init_x_frac(m, K, m)
+        Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), b).cpu().numpy()
+        rows = np.unique(np.r_[0, 1, 127, m // 2, m - 1].clip(0, m - 1))
+        ref = O.base_tcsc(np.ascontiguousarray(Xn[rows]), O.TCSC(*arrs, K, N), b.cpu().numpy())
+        assert _bits_eq(Y[rows], ref), (m, h.jit_width(m), h.jit_waves(m))
+    h.close()
+
+
 def test_structural_edges(tsg, oracle_mod):
     """All-zero W, fully dense ternary W, empty and full columns, K=0."""
     O = oracle_mod

@@ -265,11 +265,11 @@ def emulate(code, wcode, X, K, N):
     return Y[:M, :N]
 
 
-def _check(tsg, O, M, K, N, s, seed, frac, W=None, width=64):
+def _check(tsg, O, M, K, N, s, seed, frac, W=None, width=64, waves=8):
     W = O.gen_ternary(K, N, s, seed) if W is None else W
     t = O.tcsc_encode(W)
-    code, wcode = tsg.jit_codegen(*t.arrays, K, N, width=width)
-    assert Geom(code).nw == width
+    code, wcode = tsg.jit_codegen(*t.arrays, K, N, width=width, waves=waves)
+    assert Geom(code).nw == width and Geom(code).waves == waves
     X = O.init_x_frac(M, K, seed + 1) if frac else O.init_x_int(M, K, seed + 1)
     b = np.linspace(-2, 3, N).astype(np.float32)
     Y = emulate(code, wcode, X, K, N) + b
@@ -297,6 +297,16 @@ def test_jit_code_narrow_streams(tsg, oracle_mod, M, K, N, s, width):
         _check(tsg, oracle_mod, M, K, N, s, 5 + K + N + width, frac, width=width)
 
 
+@pytest.mark.parametrize("width", [32, 16, 8])
+@pytest.mark.parametrize("M,K,N,s", [(5, 70, 33, 2), (130, 300, 150, 4), (3, 97, 9, 16)])
+def test_jit_code_four_wave_workgroups(tsg, oracle_mod, M, K, N, s, width):
+    """4-wave workgroups (mid-M shapes, lib/tsg_jit_w<nw>_4w.co): each wave
+    stages 12 of the chunk's 48 pair rows, the register contract shifts
+    (lane*128 v120, accumulators from v122), twice the column tiles; same order."""
+    for frac in (False, True):
+        _check(tsg, oracle_mod, M, K, N, s, 7 + K + N + width, frac, width=width, waves=4)
+
+
 def test_jit_width_rejected(tsg, oracle_mod):
     O = oracle_mod
     t = O.tcsc_encode(O.gen_ternary(64, 20, 4, 1))
@@ -305,6 +315,10 @@ def test_jit_width_rejected(tsg, oracle_mod):
     blk = O.blocked_tcsc_encode(O.gen_ternary(64, 20, 4, 1), 16)
     with pytest.raises(tsg.TSGError, match="BlockedTCSC"):
         tsg.jit_codegen(*blk, 64, 20, B=16, width=16)
+    with pytest.raises(tsg.TSGError, match="waves"):
+        tsg.jit_codegen(*t.arrays, 64, 20, width=64, waves=4)  # 64-wide streams: 8 waves only
+    with pytest.raises(tsg.TSGError, match="waves"):
+        tsg.jit_codegen(*t.arrays, 64, 20, width=16, waves=2)
 
 
 def test_jit_code_dense_and_empty_columns(tsg, oracle_mod):
