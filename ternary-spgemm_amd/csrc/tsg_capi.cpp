@@ -75,6 +75,7 @@ struct tsg_tcsc {
     float *d_x = nullptr, *d_b = nullptr, *d_y = nullptr, *d_alpha = nullptr;
     size_t x_bytes = 0, y_bytes = 0;
     hipStream_t stream = nullptr;         // stream of the host-pointer path
+    std::mutex host_mu;                   // one host-pointer call at a time (its staging buffers)
     // timing of the main kernel
     bool timing = false;
     static constexpr int kRing = 256;     // event pairs in flight before a harvest blocks
@@ -527,6 +528,9 @@ int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, fl
     if (M == 0 || N == 0) return TSG_OK;
     if (!Y || !b || (K > 0 && !X) || (prelu && !alpha)) return fail(TSG_ERR_ARG, "null host pointer");
     DeviceGuard g(h->device);
+    // the staging buffers and the stream are the handle's: a second host thread
+    // waits here until this call's Y is back (run_dev takes h->mu inside)
+    std::lock_guard<std::mutex> lk(h->host_mu);
     const size_t xb = (size_t)M * K * sizeof(float), yb = (size_t)M * N * sizeof(float);
     if (xb > h->x_bytes) {
         if (h->d_x) HIP_TRY(hipFree(h->d_x));

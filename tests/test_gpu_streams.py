@@ -80,6 +80,39 @@ def test_threads_one_handle(tsg, oracle_mod):
     h.close()
 
 
+def test_threads_host_pointer_calls(tsg, oracle_mod):
+    """Two host threads call the synchronous host-pointer comp_func
+    (tcsc_hip_gemm, main.cpp:214-216) on one handle with different X and M:
+    the handle's staging buffers serve one call at a time."""
+    O = oracle_mod
+    K, N = 700, 900
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 23))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    bn = np.full(N, 2.0, np.float32)
+    Ms = (257, 33)  # different M: the staging buffers grow while the other thread runs
+    Xs = [O.init_x_frac(Ms[i], K, 40 + i) for i in range(2)]
+    res, err = [None, None], []
+
+    def work(i):
+        try:
+            Y = np.empty((Ms[i], N), np.float32)
+            for _ in range(6):
+                h(Xs[i], bn, Y, Ms[i], N, K)
+            res[i] = Y.copy()
+        except Exception as e:  # surfaced below
+            err.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not err, err
+    for i in range(2):
+        assert np.array_equal(res[i].view(np.uint32), O.base_tcsc(Xs[i], t, bn).view(np.uint32))
+    h.close()
+
+
 @pytest.mark.parametrize("M", [4096, 96])
 def test_graph_capture_after_reserve(tsg, oracle_mod, M):
     """tcsc_hip_reserve(max_M) prepares every width a call with M <= max_M runs;
