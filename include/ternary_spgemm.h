@@ -93,7 +93,9 @@ void tcsc_hip_destroy(tsg_tcsc *h);
  * (cpp_impl/common.h:12) bound to BaseTCSC<float> (comp.h:25-69).
  * Argument order M, N, K as there.  HOST pointers: X is M x K row-major,
  * b has N floats, Y is M x N row-major and is fully overwritten.
- * Synchronous: Y is valid on return (main.cpp:214-216, perf.cpp:62-66). */
+ * Synchronous: Y is valid on return (main.cpp:214-216, perf.cpp:62-66).
+ * Host threads sharing a handle run their host-pointer calls one at a time
+ * (the handle's staging buffers and stream). */
 int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K);
 
 /* DEVICE pointers (on the handle's device), enqueued on `stream`
