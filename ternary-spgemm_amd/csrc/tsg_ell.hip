@@ -542,6 +542,32 @@ int launch_pc_t(const float *X, const uint4 *ent, const uint2 *tab, const float 
 
 }  // namespace
 
+namespace {
+
+// Phase length E (entries of every chain per barrier).  64 while every
+// workgroup is resident at once (M * ceil(N / 64) <= 256: one per CU) and its
+// larger ring fits beside the X chunk: half the barriers, and the wider
+// producer set keeps more gathers in flight (M = 1: K = N = 16384 37.7 vs
+// 42.2 us, K = N = 4096 13.5 vs 14.2 us); else 32 (M = 2 at N = 16384, 512
+// workgroups: 20.0 vs 26.4 us with E = 64; profiles/r02_pc_phase_ab.txt).
+// TSG_ELL_PC_E=16/32/64 forces one (A/B sweeps; 32 when the forced ring does
+// not fit).  Availability (tsg_capi.cpp ell_pc_available) is judged at E = 32.
+int pc_phase(int M, int N, int C)
+{
+    static const int env = [] {
+        const char *v = getenv("TSG_ELL_PC_E");
+        const int x = v ? atoi(v) : 0;
+        return x == 16 || x == 32 || x == 64 ? x : 0;
+    }();
+    const bool fits64 = pc_lds<1, 64>(C) <= kLdsBytes, fits16 = pc_lds<1, 16>(C) <= kLdsBytes;
+    if (env == 64) return fits64 ? 64 : 32;
+    if (env) return env == 16 && fits16 ? 16 : 32;
+    const int64_t wgs = (int64_t)M * ((N + 63) / 64);
+    return wgs <= 256 && fits64 ? 64 : 32;
+}
+
+}  // namespace
+
 // 1-row tiles only: with 4 rows the ring's extra write and read of every row
 // value make the walk LDS-bound (39 vs 22.5 us at M = 4, K = 4096, N = 16384;
 // profiles/r02x_ell_pc.txt)
@@ -558,7 +584,11 @@ int launch_tcsc_ell_pc(int variant, const float *X, const uint32_t *ent, const u
     hipStream_t s = (hipStream_t)stream;
     const uint4 *e = reinterpret_cast<const uint4 *>(ent);
     const uint2 *t = reinterpret_cast<const uint2 *>(tab);
-    return launch_pc_t<1, 32>(X, e, t, b, alpha, Y, M, N, K, C, prelu, s);  // 1 consumer + 4 producer waves
+    switch (pc_phase(M, N, C)) {
+    case 16: return launch_pc_t<1, 16>(X, e, t, b, alpha, Y, M, N, K, C, prelu, s);
+    case 64: return launch_pc_t<1, 64>(X, e, t, b, alpha, Y, M, N, K, C, prelu, s);
+    default: return launch_pc_t<1, 32>(X, e, t, b, alpha, Y, M, N, K, C, prelu, s);  // 1 consumer + 4 producer waves
+    }
 }
 
 int launch_tcsc_ell(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
