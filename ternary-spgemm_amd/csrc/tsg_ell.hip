@@ -413,11 +413,16 @@ __global__ __launch_bounds__(64 * (MT + E / 8)) void tsg_tcsc_ell_pc_kernel(
         Y[(size_t)(m0 + r) * N + n] = v;
     } else {
         const uint32_t base = (uint32_t)(uintptr_t)(lds_f *)xs;
-        // the block's 8 entries, all MT rows each (one LDS read per entry),
-        // written as 4-entry runs of each of the column's MT chains
-        auto fill = [&](int ph, const uint4 e) {
+        // A block's 8 entries, all MT rows each (one LDS read per entry), are
+        // gathered into registers one interval before they are written to the
+        // ring as 4-entry runs of each of the column's MT chains: in interval
+        // k a producer writes phase k + 2 (gathered in interval k - 1), waits
+        // for those writes only, then issues the gathers of phase k + 3 and
+        // meets the barrier without waiting for them, so the gathers' latency
+        // and the LDS burst they cause overlap the barrier and the next
+        // interval instead of lengthening this one.
+        auto gather = [&](const uint4 e, float (&x)[8][MT]) {
             const uint32_t w[4] = {e.x, e.y, e.z, e.w};
-            float x[8][MT];
 #pragma unroll
             for (int h = 0; h < 8; h++) {
                 const uint32_t a = (h & 1) ? ent_addr_hi(w[h >> 1], base) : ent_addr_lo(w[h >> 1], base);
@@ -428,6 +433,8 @@ __global__ __launch_bounds__(64 * (MT + E / 8)) void tsg_tcsc_ell_pc_kernel(
                     x[h][0] = *(lds_f *)(uintptr_t)a;
                 }
             }
+        };
+        auto put = [&](int ph, const float (&x)[8][MT]) {
             float4 *dst = ring + ((size_t)(ph % 3) * (E / 4) + 2 * pj) * CH + lane * MT;
 #pragma unroll
             for (int rr = 0; rr < MT; rr++) {
@@ -435,28 +442,63 @@ __global__ __launch_bounds__(64 * (MT + E / 8)) void tsg_tcsc_ell_pc_kernel(
                 dst[CH + rr] = make_float4(x[4][rr], x[5][rr], x[6][rr], x[7][rr]);
             }
         };
-        fill(0, q[0]);
+        // after a put: its ring writes complete (s_waitcnt lgkmcnt(0) with
+        // vmcnt/expcnt not waited: the index loads stay in flight); the
+        // gathers issued after it read only the X chunk, so the interval's
+        // barrier does not wait for them
+        auto writes_done = [&]() {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto end_interval = [&]() {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        float xa[8][MT], xb[8][MT];
+        gather(q[0], xa);
+        put(0, xa);
         q[0] = load(D);
-        fill(1, q[1]);
+        gather(q[1], xb);
+        put(1, xb);
         q[1] = load(D + 1);
-        lds_barrier();
-        // phase k + 2 during phase k: whole groups of D refill their slots
-        // (no exit branch between a load and its use), the rest comes from
-        // the ring with no loads
+        gather(q[2], xa);  // phase 2, written in interval 0
+        q[2] = load(D + 2);
+        lds_barrier();     // phases 0 and 1 are in the ring (full wait: the gathers of phase 2 included)
+        // interval k: put phase k + 2 (in x[k % 2]), gather phase k + 3 into
+        // x[(k + 1) % 2]; whole groups of D refill their index slots (no exit
+        // branch between a load and its use), the rest runs without loads
         int k = 0;
         for (; k + D <= nph; k += D) {
 #pragma unroll
             for (int d = 0; d < D; d++) {
-                fill(k + d + 2, q[(d + 2) % D]);
-                q[(d + 2) % D] = load(k + d + 2 + D);
-                lds_barrier();
+                if (d % 2 == 0) {
+                    put(k + d + 2, xa);
+                    writes_done();
+                    gather(q[(d + 3) % D], xb);
+                } else {
+                    put(k + d + 2, xb);
+                    writes_done();
+                    gather(q[(d + 3) % D], xa);
+                }
+                q[(d + 3) % D] = load(k + d + 3 + D);
+                end_interval();
             }
         }
 #pragma unroll
         for (int d = 0; d < D; d++) {
             if (k + d >= nph) break;
-            fill(k + d + 2, q[(d + 2) % D]);
-            lds_barrier();
+            if (d % 2 == 0) {
+                put(k + d + 2, xa);
+                writes_done();
+                gather(q[(d + 3) % D], xb);
+            } else {
+                put(k + d + 2, xb);
+                writes_done();
+                gather(q[(d + 3) % D], xa);
+            }
+            end_interval();
         }
     }
 }
