@@ -587,8 +587,10 @@ int launch_pc_t(const float *X, const uint4 *ent, const uint2 *tab, const float 
 namespace {
 
 // Phase length E (entries of every chain per barrier).  64 while every
-// workgroup is resident at once (M * ceil(N / 64) <= 256: one per CU) and its
-// larger ring fits beside the X chunk: half the barriers, and the wider
+// workgroup is resident at once (M * ceil(N / 64) <= 256: one per CU), the
+// chains are long (K >= 2048; at K = 512-1024 the 9-wave workgroup costs more
+// than it saves: (1, 512, 2048) 6.5 vs 7.1 us, profiles/r02_ref_cases_final.jsonl)
+// and its larger ring fits beside the X chunk: half the barriers, and the wider
 // producer set keeps more gathers in flight (M = 1: K = N = 16384 37.7 vs
 // 42.2 us, K = N = 4096 13.5 vs 14.2 us); else 32 (M = 2 at N = 16384, 512
 // workgroups: 20.0 vs 26.4 us with E = 64; profiles/r02_pc_phase_ab.txt).
@@ -605,7 +607,7 @@ int pc_phase(int M, int N, int C)
     if (env == 64) return fits64 ? 64 : 32;
     if (env) return env == 16 && fits16 ? 16 : 32;
     const int64_t wgs = (int64_t)M * ((N + 63) / 64);
-    return wgs <= 256 && fits64 ? 64 : 32;
+    return wgs <= 256 && C >= 2048 && fits64 ? 64 : 32;
 }
 
 }  // namespace
