@@ -246,6 +246,12 @@ int tsg_jit_codegen_wv(const int32_t *col_start_pos, const int32_t *col_start_ne
                        int B, int width, int waves, uint32_t *code, int64_t code_cap, int64_t *code_len,
                        uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
 
+/* The weight-compiled kernel's tile map (tsg_jit_map.h): workgroup id L of a
+ * grid of mtiles x ntiles -> (column tile *nt, M tile *mt) for groups of gn
+ * column tiles x gm M tiles per XCD.  Host only (tests check it is a
+ * bijection for every shape the library launches). */
+int tsg_jit_tile_map(int L, int mtiles, int ntiles, int gn, int gm, int *nt, int *mt);
+
 /* Checks BlockedTCSC<B> arrays (layout as tcsc_hip_create_blocked): monotone
  * column starts, every row inside its block, ascending, no row both +1 and -1. */
 int tsg_blocked_tcsc_validate(const int32_t *col_start_pos, const int32_t *col_start_neg,

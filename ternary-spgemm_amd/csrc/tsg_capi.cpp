@@ -255,6 +255,23 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
     return full ? best : most;
 }
 
+// Tile map groups (tsg_jit_map.h) per call: gn column tiles x gm M tiles per
+// XCD group.  2 x 16 keeps the CU pairs that share an instruction cache on one
+// code stream (configs[2]: 1.24-1.25 ms vs 1.26-1.28 at 4 x 8; (64000, 16384,
+// 4096): 27.0 vs 28.0-28.7 ms); with at most 4 column tiles or 8 M tiles,
+// 4 x 8 (every column tile, or every M tile, of the XCD's group shares its
+// X^T chunks or code): (16000, 8192, 2048) 1.19-1.21 vs 1.31-1.34 ms,
+// (1024, 4096, 16384) 0.311-0.313 vs 0.319-0.323 ms
+// (profiles/r02_jit_map_bench_ab.txt).  TSG_JIT_GN / TSG_JIT_GM override (A/B).
+void pick_jit_map(int mtiles, int ntiles, int &gn, int &gm)
+{
+    static const int env_gn = [] { const char *e = getenv("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
+    static const int env_gm = [] { const char *e = getenv("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
+    const bool small = ntiles <= 4 || mtiles <= 8;
+    gn = env_gn > 0 ? env_gn : small ? 4 : 2;
+    gm = env_gm > 0 ? env_gm : small ? 8 : 16;
+}
+
 // Compiles and loads the image of one shape (registration, or the first call
 // that picks it).  Caller holds h->mu (or owns h exclusively).
 int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves)
@@ -495,9 +512,11 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         slot = h->ring_head;
         HIP_TRY(hipEventRecord(h->ev0[slot], s));
     }
+    int gn = 2, gm = 16;
+    if (h->kind == tsg_tcsc::kJit) pick_jit_map(Mp / tsg::kJitTileM, jv->Npad / (jv->nw * jv->waves), gn, gm);
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
-                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves, jv->waves, s)
+                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves, jv->waves, gn, gm, s)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)

@@ -23,6 +23,7 @@
 #include <iterator>
 
 #include "tsg_internal.h"
+#include "tsg_jit_map.h"
 #include "../../include/ternary_spgemm.h"
 
 namespace tsg {
@@ -553,12 +554,12 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status)
 
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
-                    uint32_t *status, int tile_cols, int waves, void *stream)
+                    uint32_t *status, int tile_cols, int waves, int gn, int gm, void *stream)
 {
     int mtiles = Mp / kJitTileM, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
-                      (void *)&status};
+                      (void *)&status, (void *)&gn, (void *)&gm};
     hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.function, (unsigned)(mtiles * ntiles), 1, 1,
                                          (unsigned)waves * 64u, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;
@@ -602,6 +603,17 @@ extern "C" int tsg_jit_codegen_wv(const int32_t *csp, const int32_t *csn, const 
     }
     if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);
     if (wcode) std::memcpy(wcode, img.wcode.data(), img.wcode.size() * 4);
+    return TSG_OK;
+}
+
+extern "C" int tsg_jit_tile_map(int L, int mtiles, int ntiles, int gn, int gm, int *nt, int *mt)
+{
+    if (!nt || !mt || mtiles <= 0 || ntiles <= 0 || gn <= 0 || gm <= 0 || L < 0 ||
+        (int64_t)L >= (int64_t)mtiles * ntiles) {
+        g_tsg_host_err = "tsg_jit_tile_map: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    tsg_jit_tile(L, mtiles, ntiles, gn, gm, *nt, *mt);
     return TSG_OK;
 }
 

@@ -42,6 +42,8 @@
 
 #include <cstdint>
 
+#include "tsg_jit_map.h"
+
 namespace {
 
 // TSG_JIT_NW: a narrower stream width (32, 16 or 8 columns per wave;
@@ -120,7 +122,7 @@ extern "C" __global__ __launch_bounds__(64) void tsg_jit_probe(uint32_t *__restr
 extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
-    int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status)
+    int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm)
 {
     __shared__ __attribute__((aligned(16))) char lds[kJRing * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -145,29 +147,10 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
         return;
     }
 
-    // XCD-aware bijective remap: each XCD gets a contiguous run of workgroup
-    // ids (blocks b and b+8 share an XCD), and consecutive ids walk groups of
-    // kGN column tiles x kGM M tiles, so the ~32 workgroups an XCD runs at once
-    // share kGN code streams and kGM X^T slabs through its L2 instead of 1 and
-    // 32 (traffic beyond L2 = kGN x code + kGM x slab per round).
-    // Measured placement (scripts/hwid_micro.hip): an XCD's slot s goes to
-    // shader engine s % 4 (rotated), CU s / 4 of it, so nt = slot % kGN puts
-    // every CU of an SE on the same column tile: the CU pairs that share an
-    // instruction cache fetch one code stream (kGN = 8 splits them: +25%).
-    // kGN = 2 (two SEs per tile) measured 4-6% faster than 4 (profiles/r01c_ab_mapping.txt).
-#ifndef TSG_JIT_GN
-#define TSG_JIT_GN 2
-#endif
-#ifndef TSG_JIT_GM
-#define TSG_JIT_GM 16
-#endif
-    constexpr int kGN = TSG_JIT_GN, kGM = TSG_JIT_GM;
-    const int T = mtiles * ntiles, L = blockIdx.x;
-    const int xcd = L & 7, slot = L >> 3, q8 = T >> 3, r8 = T & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-    const int cb = wg / (kGN * mtiles), wc = min(kGN, ntiles - kGN * cb);  // column-tile block
-    const int loc = wg - cb * kGN * mtiles, g = loc / (wc * kGM), i = loc - g * wc * kGM;
-    const int nt = kGN * cb + i % wc, mt = kGM * g + i / wc;
+    // tile map (tsg_jit_map.h): gn column tiles x gm M tiles per XCD group,
+    // chosen per call by the host (tsg_capi.cpp pick_jit_map)
+    int nt, mt;
+    tsg_jit_tile(blockIdx.x, mtiles, ntiles, gn, gm, nt, mt);
     const int m0 = mt * kJTileM;
     const int stream = wave;  // the wave's column stream
     const int ncol0 = nt * kJTileCols + stream * kJNW;

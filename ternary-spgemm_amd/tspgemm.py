@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = (
     "tsg_csc_packed_to_tcsc", "tsg_jit_codegen", "tcsc_hip_kernel_name", "tcsc_hip_encode_dense_dev",
     "tcsc_hip_create_blocked", "tsg_jit_codegen_blocked", "tsg_blocked_tcsc_validate",
     "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tcsc_hip_jit_waves", "tsg_jit_codegen_w", "tsg_jit_codegen_wv",
-    "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build",
+    "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
 )
 
 
@@ -128,6 +128,7 @@ def lib() -> C.CDLL:
     L.tcsc_hip_call_kernel.restype = C.c_char_p
     L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
                                 vp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.tsg_jit_tile_map.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.tcsc_hip_jit_width.argtypes = [H, C.c_int]
     L.tcsc_hip_jit_waves.argtypes = [H, C.c_int]
     L.tcsc_hip_set_jit_width.argtypes = [H, C.c_int]
@@ -243,6 +244,14 @@ def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0, width: int = 64,
                                 nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
            "tsg_jit_codegen")
     return code, wcode
+
+
+def jit_tile_map(L: int, mtiles: int, ntiles: int, gn: int, gm: int):
+    """(column tile, M tile) of workgroup L in the weight-compiled kernel's
+    grid (tsg_jit_map.h), groups of gn column tiles x gm M tiles per XCD."""
+    nt, mt = C.c_int(), C.c_int()
+    _check(lib().tsg_jit_tile_map(L, mtiles, ntiles, gn, gm, C.byref(nt), C.byref(mt)), "tsg_jit_tile_map")
+    return nt.value, mt.value
 
 
 def ell_build(csp, csn, rip, rin, K: int, N: int, Cmax: int, MT: int):

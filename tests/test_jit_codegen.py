@@ -444,3 +444,19 @@ def test_kernel_descriptor_float_mode(co):
     assert (rsrc1 >> 16) & 3 == 3, "FP32 denormals must be preserved (FLOAT_DENORM_MODE_32)"
     assert (rsrc1 >> 23) & 1 == 1, "IEEE mode must be on"
 
+
+
+@pytest.mark.parametrize("gn,gm", [(2, 16), (4, 8), (1, 1), (3, 5), (8, 4)])
+def test_tile_map_is_a_bijection(tsg, gn, gm):
+    """Every workgroup of an mtiles x ntiles grid gets a distinct tile, every
+    tile gets one (tsg_jit_map.h, the dispatcher's map), for the group sizes
+    the library picks (2 x 16, 4 x 8) and odd ones, over grids that are and
+    are not multiples of the 8 XCDs and of the groups."""
+    for mtiles, ntiles in [(1, 1), (1, 7), (4, 64), (8, 32), (32, 32), (125, 4), (500, 8), (3, 3), (33, 9),
+                           (2, 129), (17, 1)]:
+        seen = set()
+        for L in range(mtiles * ntiles):
+            nt, mt = tsg.jit_tile_map(L, mtiles, ntiles, gn, gm)
+            assert 0 <= nt < ntiles and 0 <= mt < mtiles
+            seen.add((nt, mt))
+        assert len(seen) == mtiles * ntiles, (mtiles, ntiles, gn, gm)
