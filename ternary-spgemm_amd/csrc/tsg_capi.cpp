@@ -268,8 +268,8 @@ void pick_jit_map(int mtiles, int ntiles, int &gn, int &gm)
     static const int env_gn = [] { const char *e = getenv("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
     static const int env_gm = [] { const char *e = getenv("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
     const bool small = ntiles <= 4 || mtiles <= 8;
-    gn = env_gn > 0 ? env_gn : small ? 4 : 2;
-    gm = env_gm > 0 ? env_gm : small ? 8 : 16;
+    gn = std::min(env_gn > 0 ? env_gn : small ? 4 : 2, std::max(ntiles, 1));  // a group never exceeds the grid
+    gm = std::min(env_gm > 0 ? env_gm : small ? 8 : 16, std::max(mtiles, 1));
 }
 
 // Compiles and loads the image of one shape (registration, or the first call
