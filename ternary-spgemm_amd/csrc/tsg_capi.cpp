@@ -397,7 +397,11 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // M rows as M 1-row producer/consumer tiles while the M index streams stay
     // small (M = 2 at N = 16384: 20.0 vs 22.9 us; M = 4 at N = 4096: 14.7 vs
     // 21.9 us; profiles/r02z2_pc_rows.txt)
-    if (M <= 4 && (int64_t)M * h->N <= kEllPcRowsMaxMN && ell_pc_available(h)) v = 0;
+    static const int64_t pc_rows_max_mn = [] {  // TSG_ELL_PC_MAXMN: A/B sweeps of the threshold
+        const char *e = getenv("TSG_ELL_PC_MAXMN");
+        return e ? (int64_t)atoll(e) : kEllPcRowsMaxMN;
+    }();
+    if (M <= 4 && (int64_t)M * h->N <= pc_rows_max_mn && ell_pc_available(h)) v = 0;
     static const int force = [] {  // TSG_ELL_VARIANT: diagnostic sweeps only
         const char *e = getenv("TSG_ELL_VARIANT");
         return e ? atoi(e) : -1;
