@@ -7,7 +7,7 @@ HBM) -> Y [M,N] through the C-ABI (tcsc_hip_gemm_dev: X^T staging kernel +
 the TCSC kernel).  Workload at N=1 = BASELINE.json configs[2]
 (M=4096 K=4096 N=16384 s=4).
 
-Multi-GPU (torchrun, one process per GPU, RCCL): W's columns are sharded
+Multi-GPU (one process per GPU, RCCL): W's columns are sharded
 (tsg_dist.py).  `value` is the compute step (every rank's Y column block, no
 collective on the compute path); for world > 1 the line also carries the
 RCCL all-gather of the Y blocks into the row-major [M, N] result:
@@ -16,6 +16,15 @@ compute + gather pipelined by M chunks, tsg_dist.GatherPipeline).
   * default (weak): every rank owns --N columns (N_total = N * P; P = 8 is
     configs[4], N = 131072); each rank draws only its own column block.
   * --strong: N_total = --N fixed, N/P columns per rank (same W for every P).
+
+Launch: under torchrun (WORLD_SIZE set) this process is one rank, and
+WORLD_SIZE must equal --gpus.  Without WORLD_SIZE and with --gpus N > 1 this
+process is only the launcher: it starts N rank processes (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT) before anything touches the
+GPU, forwards rank 0's JSON line, and exits non-zero if a rank fails or the
+world that ran differs from --gpus.  A rank whose LOCAL_RANK has no GPU fails
+(RCCL), except in the one-GPU rehearsal TSG_BENCH_BACKEND=gloo, where ranks
+share the visible devices.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
 """
@@ -96,9 +105,10 @@ def cpu_baseline(X, csp, csn, rip, rin, K, N, s, Y_gpu, rows1):
     Xh = X.cpu().numpy()
     nnz = len(rip) + len(rin)
     legs = []
+    omp_name = f"BaseTCSC_omp{threads}"
     for name, kern, th, rows in (("BaseTCSC", "BaseTCSC", 1, rows1),
                                  ("DoubleUnrolledTCSC_K4_M4", "DoubleUnrolledTCSC_K4_M4", 1, rows1),
-                                 ("BaseTCSC_omp", "BaseTCSC_omp", threads, M)):
+                                 (omp_name, "BaseTCSC_omp", threads, M)):
         rows = min(rows, M)
         Xs = np.ascontiguousarray(Xh[:rows])
         sec, runs, cyc, Yc = O.perf_calibrated(kern, Xs, tc, bs, threads=th if kern.endswith("omp") else 0)
@@ -108,36 +118,152 @@ def cpu_baseline(X, csp, csn, rip, rin, K, N, s, Y_gpu, rows1):
                      "tsc_cycles_per_call": round(cyc), "flops_per_tsc_cycle": round(T.flops(rows, N, nnz) / cyc, 4),
                      "bit_identical_to_gpu_rows": same,
                      "source": {"BaseTCSC": "comp.h:25-69", "DoubleUnrolledTCSC_K4_M4": "comp.h:1227-1438",
-                                "BaseTCSC_omp": "comp.h:25-69 + OpenMP over rows (our parallelisation)"}[name]})
+                                omp_name: f"comp.h:25-69 + OpenMP over rows on {threads} threads (our "
+                                          f"parallelisation; OMP_NUM_THREADS={host['omp_num_threads_env']}: "
+                                          f"the box's CPU share, of {host['cpus_in_affinity']} CPUs in "
+                                          f"affinity)"}[name]})
     base = legs[0]
     return {"value": base["value"], "unit": "GFLOP/s", "cores": 1, "kind": "port",
             "sample": (f"BaseTCSC restatement (oracle/tcsc_oracle.c, comp.h:25-69), first {base['rows']} of {M} rows, "
                        f"K={K} N={N} s={s}, gcc -O3 -fno-tree-vectorize, timed as perf.cpp:37-71 "
                        f"(rdtsc, calibrated to >= 1e8 cycles, {base['runs']} run(s) of {base['sec_per_call']} s); "
                        f"legs: 1-thread BaseTCSC, 1-thread DoubleUnrolledTCSC<4,4> (the reference's best), "
-                       f"BaseTCSC + OpenMP on {threads} threads over all {M} rows"),
+                       f"BaseTCSC + OpenMP on {threads} threads (the box's CPU share; "
+                       f"{host['cpus_in_affinity']} CPUs in affinity) over all {M} rows"),
             "host": host, "legs": legs}
+
+
+def launch_mode(gpus: int, env) -> str:
+    """'rank': this process is one rank (torchrun, a launched rank, or N = 1);
+    'launch': start `gpus` rank processes (no WORLD_SIZE and gpus > 1)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    return "rank" if "WORLD_SIZE" in env or gpus == 1 else "launch"
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a) -> int:
+    """Start --gpus rank processes of this script (one per GPU) and wait for
+    them.  Runs before any torch / HIP call in this process: the ranks are
+    children (never an exec of this process).  Rank 0's stdout (the JSON
+    line) is forwarded after checking its n_gpus; every other output goes to
+    stderr.  If a rank fails, the others are terminated (by PID) and the
+    failing exit code is returned."""
+    import subprocess
+    import threading
+    n = a.gpus
+    port = _free_port()
+    dry = os.environ.get("TSG_BENCH_DRYRUN") == "1"
+    procs, outs = [], [[] for _ in range(n)]
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        piped = r == 0 or dry
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if piped else sys.stderr, text=True))
+    readers = []
+    for r, p in enumerate(procs):
+        if p.stdout is not None:
+            t = threading.Thread(target=lambda p=p, o=outs[r]: o.extend(p.stdout), daemon=True)
+            t.start()
+            readers.append(t)
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]  # every rank, every round (no short-circuit)
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            # a failed rank leaves the others waiting in the rendezvous or a
+            # collective: stop them (SIGTERM, then SIGKILL), by PID
+            rc = bad[0]
+            print(f"bench.py: a rank exited with {rc}; terminating the others", file=sys.stderr)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            t_end = time.time() + 10
+            while time.time() < t_end and any(p.poll() is None for p in procs):
+                time.sleep(0.1)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        if all(c is not None for c in codes):
+            break
+        time.sleep(0.2)
+    for t in readers:
+        t.join(timeout=10)
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    if dry:
+        for r in range(n):
+            sys.stdout.write("".join(outs[r]))
+        return rc
+    lines = [ln for ln in outs[0] if ln.strip()]
+    for ln in lines[:-1]:
+        sys.stderr.write(ln)
+    if rc != 0:
+        print(f"bench.py: rank failure (exit {rc}) with --gpus {n}", file=sys.stderr)
+        return rc
+    if not lines:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    try:
+        ran = json.loads(lines[-1]).get("n_gpus")
+    except ValueError:
+        ran = None
+    if ran != n:
+        sys.stderr.write(lines[-1])
+        print(f"bench.py: --gpus {n} but the run reported n_gpus={ran}", file=sys.stderr)
+        return 1
+    sys.stdout.write(lines[-1])
+    sys.stdout.flush()
+    return 0
 
 
 def main():
     a = parse()
-    import torch
-    import torch.distributed as dist
-
+    if launch_mode(a.gpus, os.environ) == "launch":
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and rank == 0:
-        print(f"# note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    # one process per GPU; the modulo only matters for a multi-rank rehearsal
-    # on a box with fewer GPUs (TSG_BENCH_BACKEND=gloo: RCCL refuses two ranks
-    # on one device)
-    local = local % max(torch.cuda.device_count(), 1)
+    if world != a.gpus:
+        # a 1-GPU line under an N-GPU request is never reported
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("TSG_BENCH_DRYRUN") == "1":  # launcher test (tests/test_bench_launch.py): no GPU
+        if os.environ.get("TSG_BENCH_DRYRUN_FAIL_RANK") is not None:
+            # a failing rank while the others wait (as in a rendezvous)
+            if rank == int(os.environ["TSG_BENCH_DRYRUN_FAIL_RANK"]):
+                sys.exit(3)
+            time.sleep(600)
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
+    import torch
+    import torch.distributed as dist
+
+    backend = os.environ.get("TSG_BENCH_BACKEND", "nccl") if world > 1 else None
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        # one process per GPU; only the one-GPU rehearsal (gloo: RCCL refuses
+        # two ranks on one device) shares the visible devices between ranks
+        if backend != "gloo" or ndev == 0:
+            print(f"bench.py: rank {rank} has LOCAL_RANK {local} but {ndev} GPU(s) are visible "
+                  f"(--gpus {a.gpus}); TSG_BENCH_BACKEND=gloo rehearses several ranks per GPU",
+                  file=sys.stderr)
+            sys.exit(3)
+        local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    backend = None
     if world > 1:
-        backend = os.environ.get("TSG_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -153,7 +279,7 @@ def main():
     t0 = time.time()
     csp, csn, rip, rin = D.ShardedTCSC.draw(K, Ntot, s, a.seed_w, rank, world, mode)
     h = T.TCSCDevice(csp, csn, rip, rin, K, Nr, device=local)
-    kname = h.kernel_name()
+    kname = h.call_kernel(M)  # the kernel THIS call launches (small M runs the ELL walks)
     nnz = int(len(rip) + len(rin))
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed_x)
@@ -262,13 +388,24 @@ def main():
     if rank == 0 and world == 1:
         Xh, bh = X.cpu().numpy(), b.cpu().numpy()
         Yh = np.empty((M, Nr), np.float32)
-        h(Xh, bh, Yh, M, Nr, K)
-        reps = 3
-        e0 = time.perf_counter()
-        for _ in range(reps):
+        Yref = Y.cpu().numpy()
+
+        def host_ms(chunks, reps=5):
+            h.set_host_chunks(chunks)
             h(Xh, bh, Yh, M, Nr, K)
-        e_ms = (time.perf_counter() - e0) / reps * 1e3
+            ts = []
+            for _ in range(reps):
+                e0 = time.perf_counter()
+                h(Xh, bh, Yh, M, Nr, K)
+                ts.append((time.perf_counter() - e0) * 1e3)
+            same = bool(np.array_equal(Yh.view(np.uint32), Yref.view(np.uint32)))
+            return float(np.median(ts)), same
+
+        serial_ms, serial_ok = host_ms(1)
+        e_ms, e_ok = host_ms(0)  # the default: M-chunk pipeline
         e2e = {"ms": round(e_ms, 3), "gflops": round(T.flops(M, Nr, nnz) / (e_ms * 1e-3) / 1e9, 1),
+               "chunk_rows": h.host_chunk_rows(M), "unpipelined_ms": round(serial_ms, 3),
+               "bit_identical_to_device_call": e_ok and serial_ok, "timing": "median of 5 calls",
                "bytes_over_pcie": 4 * (M * K + Nr + M * Nr)}
 
     # --- CPU baseline (rank 0 at N=1 only): bounded samples of the same workload

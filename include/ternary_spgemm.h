@@ -95,8 +95,20 @@ void tcsc_hip_destroy(tsg_tcsc *h);
  * b has N floats, Y is M x N row-major and is fully overwritten.
  * Synchronous: Y is valid on return (main.cpp:214-216, perf.cpp:62-66).
  * Host threads sharing a handle run their host-pointer calls one at a time
- * (the handle's staging buffers and stream). */
+ * (the handle's staging buffers and streams).
+ * A large call is pipelined by M chunks (tcsc_hip_host_chunk_rows): X chunk
+ * i+1 travels in while chunk i computes and chunk i-1's Y travels out, on
+ * three streams of the handle plus one helper thread for the Y copies; the
+ * result is the unchunked one bit for bit (rows are independent). */
 int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K);
+
+/* Host-pointer pipeline chunks: 0 = automatic (one per ~32 MiB of Y, at most
+ * 16, >= 256 rows, multiples of 128; small-M calls whole), or force n chunks
+ * (1 = no pipeline; tests and A/B).  tcsc_hip_host_chunk_rows: rows per chunk
+ * a call with M rows uses (M = unchunked).  Extension: no reference
+ * counterpart. */
+int tcsc_hip_set_host_chunks(tsg_tcsc *h, int chunks);
+int tcsc_hip_host_chunk_rows(tsg_tcsc *h, int M);
 
 /* DEVICE pointers (on the handle's device), enqueued on `stream`
  * (a hipStream_t; NULL = legacy default stream); returns without waiting.
@@ -105,10 +117,15 @@ int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, 
  * previous call waits (hipStreamWaitEvent) for the previous call's kernel
  * before it overwrites that buffer, so calls from several streams / threads
  * on one handle are safe (and run one after the other on the device).
+ * The first call whose M picks a code image or work-buffer size the handle
+ * has not prepared yet compiles / allocates it and synchronises `stream`
+ * (the image's probe launch); tcsc_hip_reserve(h, max_M) is the place to do
+ * that ahead of time.
  * Graph capture: after tcsc_hip_reserve(h, max_M), calls with M <= max_M
  * allocate, compile and synchronise nothing and can be captured; a captured
  * call reuses the work buffer when replayed, so a replay must not overlap
- * other calls on the same handle issued on other streams. */
+ * other calls on the same handle issued on other streams (a capture does not
+ * change what uncaptured calls on other streams wait for). */
 int tcsc_hip_gemm_dev(tsg_tcsc *h, const float *dX, const float *db, float *dY,
                       int M, int N, int K, void *stream);
 

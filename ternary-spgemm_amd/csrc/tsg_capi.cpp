@@ -7,8 +7,11 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ternary_spgemm.h"
@@ -74,8 +77,14 @@ struct tsg_tcsc {
     // host-pointer path staging (tcsc_hip_gemm): grow-only
     float *d_x = nullptr, *d_b = nullptr, *d_y = nullptr, *d_alpha = nullptr;
     size_t x_bytes = 0, y_bytes = 0;
-    hipStream_t stream = nullptr;         // stream of the host-pointer path
+    hipStream_t stream = nullptr;         // stream of the host-pointer path (compute)
     std::mutex host_mu;                   // one host-pointer call at a time (its staging buffers)
+    // host-pointer pipeline (run_host): X chunks in on s_in, chunk compute on
+    // `stream`, Y chunks out on s_out; one event pair per chunk
+    static constexpr int kHostChunksMax = 16;
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    hipEvent_t ev_in[kHostChunksMax] = {}, ev_c[kHostChunksMax] = {};
+    int host_chunks = 0;                  // tcsc_hip_set_host_chunks: 0 = automatic
     // timing of the main kernel
     bool timing = false;
     static constexpr int kRing = 256;     // event pairs in flight before a harvest blocks
@@ -272,9 +281,18 @@ void pick_jit_map(int mtiles, int ntiles, int &gn, int &gm)
     gm = std::min(env_gm > 0 ? env_gm : small ? 8 : 16, std::max(mtiles, 1));
 }
 
-// Compiles and loads the image of one shape (registration, or the first call
-// that picks it).  Caller holds h->mu (or owns h exclusively).
-int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves)
+int handle_stream(tsg_tcsc *h, hipStream_t &s)
+{
+    if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    s = h->stream;
+    return TSG_OK;
+}
+
+// Compiles and loads the image of one shape (registration, tcsc_hip_reserve,
+// or the first call that picks it) and runs its probe on `s` -- the call's
+// stream, or the handle's own non-blocking stream (nullptr) -- and
+// synchronises that stream only.  Caller holds h->mu (or owns h exclusively).
+int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStream_t s = nullptr)
 {
     const int i = shape_index(nw, waves);
     if (i < 0 || !tsg::jit_width_ok(nw))
@@ -324,9 +342,18 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves)
         return fail(TSG_ERR_NOMEM, "hipMalloc of the jit status word failed");
     }
     uint32_t st[2] = {0xffffffffu, 0u};
-    bool ok = hipMemset(h->d_status, 0, 16) == hipSuccess && tsg::launch_jit_probe(v.mod, h->d_status) == 0 &&
-              hipStreamSynchronize(nullptr) == hipSuccess &&
-              hipMemcpy(st, h->d_status, sizeof st, hipMemcpyDeviceToHost) == hipSuccess;
+    if (!s) {
+        const int rs = handle_stream(h, s);
+        if (rs) {
+            (void)hipFree(v.d_wcode);
+            v.d_wcode = nullptr;
+            v.mod.unload();
+            return rs;
+        }
+    }
+    bool ok = hipMemsetAsync(h->d_status, 0, 16, s) == hipSuccess && tsg::launch_jit_probe(v.mod, h->d_status, s) == 0 &&
+              hipMemcpyAsync(st, h->d_status, sizeof st, hipMemcpyDeviceToHost, s) == hipSuccess &&
+              hipStreamSynchronize(s) == hipSuccess;
     if (!ok || st[0] != 0 || st[1] != tsg::kJitMagic0) {
         (void)hipFree(v.d_wcode);
         v.d_wcode = nullptr;
@@ -419,11 +446,22 @@ int ensure_ell(tsg_tcsc *h, int v)
                          h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, tsg::kEllMaxC[v], tsg::kEllTileM[v], e.img);
     DeviceGuard g(h->device);
     const size_t eb = e.img.ent.size() * 4, tb = std::max<size_t>(e.img.tab.size() * 4, 8);
-    if (hipMalloc(&e.d_ent, eb) != hipSuccess || hipMalloc(&e.d_tab, tb) != hipSuccess)
-        return fail(TSG_ERR_NOMEM, "hipMalloc of the small-M (ELL) image failed");
-    if (hipMemcpy(e.d_ent, e.img.ent.data(), eb, hipMemcpyHostToDevice) != hipSuccess ||
-        (!e.img.tab.empty() && hipMemcpy(e.d_tab, e.img.tab.data(), e.img.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
-        return fail(TSG_ERR_HIP, "upload of the small-M (ELL) image failed");
+    // allocate and upload into locals; the variant owns them only once both
+    // uploads succeeded (a failed attempt leaves nothing behind, a retry
+    // starts clean)
+    uint32_t *d_ent = nullptr, *d_tab = nullptr;
+    auto drop = [&](int code, const char *msg) {
+        if (d_ent) (void)hipFree(d_ent);
+        if (d_tab) (void)hipFree(d_tab);
+        return fail(code, msg);
+    };
+    if (hipMalloc(&d_ent, eb) != hipSuccess || hipMalloc(&d_tab, tb) != hipSuccess)
+        return drop(TSG_ERR_NOMEM, "hipMalloc of the small-M (ELL) image failed");
+    if (hipMemcpy(d_ent, e.img.ent.data(), eb, hipMemcpyHostToDevice) != hipSuccess ||
+        (!e.img.tab.empty() && hipMemcpy(d_tab, e.img.tab.data(), e.img.tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+        return drop(TSG_ERR_HIP, "upload of the small-M (ELL) image failed");
+    e.d_ent = d_ent;
+    e.d_tab = d_tab;
     e.bytes = (int64_t)(eb + tb);
     std::vector<uint32_t>().swap(e.img.ent);
     std::vector<uint32_t>().swap(e.img.tab);
@@ -491,7 +529,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         if (!jv->mod.function && capturing)
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(sh.nw) +
                                          " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
-        rc = ensure_jit_variant(h, sh.nw, sh.waves);
+        rc = ensure_jit_variant(h, sh.nw, sh.waves, s);
         if (rc) return rc;
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
@@ -530,11 +568,11 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         h->ring_head = (h->ring_head + 1) % tsg_tcsc::kRing;
         h->ring_count++;
     }
-    if (capturing) {
-        // a captured call's reads happen at replay time: not tracked (a replay
-        // must not overlap calls on other streams, include/ternary_spgemm.h)
-        h->work_used = false;
-    } else {
+    if (!capturing) {
+        // (a captured call's reads happen at replay time and are not tracked:
+        // a replay must not overlap calls on other streams,
+        // include/ternary_spgemm.h; the record of the last uncaptured call
+        // stays, so the next uncaptured call still waits for it)
         HIP_TRY(hipEventRecord(h->work_ev, s));
         h->work_stream = s;
         h->work_used = true;
@@ -542,6 +580,41 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     return TSG_OK;
 }
 
+// Chunks of the host-pointer pipeline: one per ~32 MiB of Y (the PCIe leg
+// that binds: Y is the largest transfer), at most kHostChunksMax, each a whole
+// number of 128-row M tiles and at least 256 rows; calls the small-M kernel
+// takes run whole.  configs[2] (268 MB of Y): 8 chunks of 512 rows.
+int host_chunk_rows(const tsg_tcsc *h, int M)
+{
+    const int64_t ybytes = (int64_t)M * h->N * 4;
+    int n = h->host_chunks > 0 ? h->host_chunks : (int)std::min<int64_t>(ybytes >> 25, tsg_tcsc::kHostChunksMax);
+    n = std::min(n, tsg_tcsc::kHostChunksMax);
+    if (n <= 1 || (h->host_chunks <= 0 && pick_ell_variant(h, M) >= 0)) return M;
+    int rows = (M + n - 1) / n;
+    rows = (rows + tsg::kJitTileM - 1) / tsg::kJitTileM * tsg::kJitTileM;
+    if (h->host_chunks <= 0) rows = std::max(rows, 256);
+    return std::min(rows, M);
+}
+
+int host_pipe_ready(tsg_tcsc *h)
+{
+    if (h->s_in) return TSG_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&h->s_out, hipStreamNonBlocking));
+    for (int i = 0; i < tsg_tcsc::kHostChunksMax; i++) {
+        HIP_TRY(hipEventCreateWithFlags(&h->ev_in[i], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->ev_c[i], hipEventDisableTiming));
+    }
+    HIP_TRY(hipStreamCreateWithFlags(&h->s_in, hipStreamNonBlocking));  // last: marks the pipeline ready
+    return TSG_OK;
+}
+
+// The comp_func call (main.cpp:214-216): host X, b, Y; synchronous.  Pipelined
+// by M chunks over three streams: the calling thread copies X chunk i in
+// (s_in) and enqueues its compute (the handle's stream, after chunk i's copy)
+// while a helper thread copies the finished Y chunks out (s_out, after each
+// chunk's compute), so the H2D of chunk i+1, the kernel of chunk i and the
+// D2H of chunk i-1 overlap (PCIe is full duplex).  Rows are independent, so
+// the chunked result is the unchunked one bit for bit.
 int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, float *Y, int M,
              int N, int K, bool prelu)
 {
@@ -551,8 +624,8 @@ int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, fl
     if (M == 0 || N == 0) return TSG_OK;
     if (!Y || !b || (K > 0 && !X) || (prelu && !alpha)) return fail(TSG_ERR_ARG, "null host pointer");
     DeviceGuard g(h->device);
-    // the staging buffers and the stream are the handle's: a second host thread
-    // waits here until this call's Y is back (run_dev takes h->mu inside)
+    // the staging buffers and the streams are the handle's: a second host
+    // thread waits here until this call's Y is back (run_dev takes h->mu inside)
     std::lock_guard<std::mutex> lk(h->host_mu);
     const size_t xb = (size_t)M * K * sizeof(float), yb = (size_t)M * N * sizeof(float);
     if (xb > h->x_bytes) {
@@ -569,14 +642,73 @@ int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, fl
         if (hipMalloc(&h->d_y, yb) != hipSuccess) return fail(TSG_ERR_NOMEM, "hipMalloc Y");
         h->y_bytes = yb;
     }
-    if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-    hipStream_t s = h->stream;
-    if (xb) HIP_TRY(hipMemcpyAsync(h->d_x, X, xb, hipMemcpyHostToDevice, s));
+    hipStream_t s = nullptr;
+    int rc = handle_stream(h, s);
+    if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(h->d_b, b, (size_t)N * sizeof(float), hipMemcpyHostToDevice, s));
     if (prelu) HIP_TRY(hipMemcpyAsync(h->d_alpha, alpha, (size_t)N * sizeof(float), hipMemcpyHostToDevice, s));
-    int rc = run_dev(h, h->d_x, h->d_b, h->d_alpha, h->d_y, M, N, K, s, prelu);
+    const int rows = host_chunk_rows(h, M);
+    if (rows >= M) {
+        if (xb) HIP_TRY(hipMemcpyAsync(h->d_x, X, xb, hipMemcpyHostToDevice, s));
+        rc = run_dev(h, h->d_x, h->d_b, h->d_alpha, h->d_y, M, N, K, s, prelu);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(Y, h->d_y, yb, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return TSG_OK;
+    }
+    rc = host_pipe_ready(h);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(Y, h->d_y, yb, hipMemcpyDeviceToHost, s));
+    const int nchunk = (M + rows - 1) / rows;
+    // chunks enqueued by this thread (their ev_c recorded); -1 = stop (error)
+    std::mutex m;
+    std::condition_variable cv;
+    int enq = 0;
+    hipError_t out_err = hipSuccess;
+    std::thread out([&] {
+        DeviceGuard tg(h->device);
+        for (int i = 0; i < nchunk && out_err == hipSuccess; i++) {
+            {
+                std::unique_lock<std::mutex> ul(m);
+                cv.wait(ul, [&] { return enq > i || enq < 0; });
+                if (enq < 0) break;
+            }
+            const size_t r0 = (size_t)i * rows, nr = std::min<size_t>(rows, (size_t)M - r0);
+            out_err = hipStreamWaitEvent(h->s_out, h->ev_c[i], 0);
+            if (out_err == hipSuccess)
+                out_err = hipMemcpyAsync(Y + r0 * N, h->d_y + r0 * N, nr * N * sizeof(float), hipMemcpyDeviceToHost,
+                                         h->s_out);
+        }
+        const hipError_t e = hipStreamSynchronize(h->s_out);
+        if (out_err == hipSuccess) out_err = e;
+    });
+    auto stop = [&](int code) {
+        {
+            std::lock_guard<std::mutex> gl(m);
+            if (code) enq = -1;
+        }
+        cv.notify_all();
+        out.join();
+        return code;
+    };
+    for (int i = 0; i < nchunk; i++) {
+        const size_t r0 = (size_t)i * rows, nr = std::min<size_t>(rows, (size_t)M - r0);
+        hipError_t e = hipSuccess;
+        if (K > 0) e = hipMemcpyAsync(h->d_x + r0 * K, X + r0 * K, nr * K * sizeof(float), hipMemcpyHostToDevice, h->s_in);
+        if (e == hipSuccess) e = hipEventRecord(h->ev_in[i], h->s_in);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, h->ev_in[i], 0);
+        if (e != hipSuccess) return stop(fail(TSG_ERR_HIP, std::string("host pipeline (X chunk): ") + hipGetErrorString(e)));
+        rc = run_dev(h, h->d_x + r0 * K, h->d_b, h->d_alpha, h->d_y + r0 * N, (int)nr, N, K, s, prelu);
+        if (rc) return stop(rc);
+        e = hipEventRecord(h->ev_c[i], s);
+        if (e != hipSuccess) return stop(fail(TSG_ERR_HIP, std::string("host pipeline (event): ") + hipGetErrorString(e)));
+        {
+            std::lock_guard<std::mutex> gl(m);
+            enq = i + 1;
+        }
+        cv.notify_all();
+    }
+    stop(0);
+    if (out_err != hipSuccess) return fail(TSG_ERR_HIP, std::string("host pipeline (Y chunk): ") + hipGetErrorString(out_err));
     HIP_TRY(hipStreamSynchronize(s));
     return TSG_OK;
 }
@@ -599,6 +731,12 @@ void free_handle(tsg_tcsc *h)
         if (e.d_tab) (void)hipFree(e.d_tab);
     }
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->s_in) (void)hipStreamDestroy(h->s_in);
+    if (h->s_out) (void)hipStreamDestroy(h->s_out);
+    for (int i = 0; i < tsg_tcsc::kHostChunksMax; i++) {
+        if (h->ev_in[i]) (void)hipEventDestroy(h->ev_in[i]);
+        if (h->ev_c[i]) (void)hipEventDestroy(h->ev_c[i]);
+    }
     for (int i = 0; i < tsg_tcsc::kRing; i++) {
         if (h->ev0[i]) (void)hipEventDestroy(h->ev0[i]);
         if (h->ev1[i]) (void)hipEventDestroy(h->ev1[i]);
@@ -702,7 +840,7 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
             // A generated image that the loader refuses (or whose probe launch
             // does not find its region) falls back to the rx kernel, unless jit
             // was asked for explicitly or the format needs it (BlockedTCSC).
-            if (rc0 != TSG_ERR_HIP || kenv || B) {
+            if ((rc0 != TSG_ERR_HIP && rc0 != TSG_ERR_RANGE) || kenv || B) {
                 free_handle(h);
                 return rc0;
             }
@@ -885,6 +1023,24 @@ extern "C" int tcsc_hip_jit_waves(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
     return pick_jit_shape(h, M).waves;
+}
+
+extern "C" int tcsc_hip_set_host_chunks(tsg_tcsc *h, int chunks)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    if (chunks < 0 || chunks > tsg_tcsc::kHostChunksMax)
+        return fail(TSG_ERR_ARG, "tcsc_hip_set_host_chunks: expected 0 (auto) .. " +
+                                     std::to_string(tsg_tcsc::kHostChunksMax));
+    std::lock_guard<std::mutex> lk(h->host_mu);
+    h->host_chunks = chunks;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_host_chunk_rows(tsg_tcsc *h, int M)
+{
+    if (!h || M <= 0) return 0;
+    std::lock_guard<std::mutex> lk(h->host_mu);
+    return host_chunk_rows(h, M);
 }
 
 extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)

@@ -123,7 +123,7 @@ struct JitModule {
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                     int prelu, uint32_t *status, int tile_cols, int waves, int gn, int gm, void *stream);
-int launch_jit_probe(const JitModule &jm, uint32_t *status);  // legacy default stream
+int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream);
 
 // ---------------------------------------------------------------------------
 // "ell" small-M kernel (tsg_tcsc_ell_kernel, tsg_ell.hip): sliced-ELL entry

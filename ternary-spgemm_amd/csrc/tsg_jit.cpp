@@ -545,10 +545,11 @@ void JitModule::unload()
     probe = nullptr;
 }
 
-int launch_jit_probe(const JitModule &jm, uint32_t *status)
+int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream)
 {
     void *params[] = {(void *)&status};
-    const hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.probe, 1, 1, 1, 64, 1, 1, 0, nullptr, params, nullptr);
+    const hipError_t e =
+        hipModuleLaunchKernel((hipFunction_t)jm.probe, 1, 1, 1, 64, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;
 }
 

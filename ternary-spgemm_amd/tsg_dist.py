@@ -171,7 +171,10 @@ class GatherPipeline:
     n0:n1] into the contiguous Y_chunk [r1-r0, w_local] on the current stream;
     the all-gather of a chunk is issued async right after its compute, so the
     collective's stream waits for that compute only and runs beside the next
-    chunk's kernel.  Buffers are allocated once (no allocation per step)."""
+    chunk's kernel.  Buffers are allocated once: the gather buffers in
+    __init__, and for an uneven shard (w_local < the widest shard) one
+    contiguous [Mc, w_local] compute buffer per chunk on the first run() --
+    no allocation per step."""
 
     def __init__(self, M: int, N: int, world: int, chunks: int = 4, device=None, dtype=None,
                  group=None):
@@ -184,18 +187,24 @@ class GatherPipeline:
         self.Yloc = [torch.zeros((r1 - r0, self.wmax), dtype=dtype, device=device) for r0, r1 in self.ranges]
         self.G = [torch.empty((world * (r1 - r0), self.wmax), dtype=dtype, device=device)
                   for r0, r1 in self.ranges]
+        self._narrow = None  # (w_local, [Mc, w_local] buffers) for an uneven shard
+
+    def _narrow_buffers(self, w_local: int):
+        if self._narrow is None or self._narrow[0] != w_local:
+            self._narrow = (w_local, [Yc.new_empty((Yc.shape[0], w_local)) for Yc in self.Yloc])
+        return self._narrow[1]
 
     def run(self, compute: Callable, Y_full, w_local: int) -> None:
         import torch.distributed as dist
         pending = []
+        narrow = self._narrow_buffers(w_local) if w_local != self.wmax else None
         for i, (r0, r1) in enumerate(self.ranges):
             Yc = self.Yloc[i]
-            if w_local == self.wmax:
+            if narrow is None:
                 compute(r0, r1, Yc)
             else:  # uneven shard: compute contiguous, pad into the gather buffer
-                tmp = Yc.new_empty((r1 - r0, w_local))
-                compute(r0, r1, tmp)
-                Yc[:, :w_local].copy_(tmp)
+                compute(r0, r1, narrow[i])
+                Yc[:, :w_local].copy_(narrow[i])
             work = _all_gather_into(self.G[i], Yc, self.group, async_op=True)
             pending.append((i, work))
             if len(pending) > 1:

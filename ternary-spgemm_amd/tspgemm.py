@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_create_blocked", "tsg_jit_codegen_blocked", "tsg_blocked_tcsc_validate",
     "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tcsc_hip_jit_waves", "tsg_jit_codegen_w", "tsg_jit_codegen_wv",
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
+    "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows",
 )
 
 
@@ -124,6 +125,8 @@ def lib() -> C.CDLL:
     L.tsg_jit_codegen_wv.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                      C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tcsc_hip_set_small_m.argtypes = [H, C.c_int]
+    L.tcsc_hip_set_host_chunks.argtypes = [H, C.c_int]
+    L.tcsc_hip_host_chunk_rows.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.restype = C.c_char_p
     L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
@@ -518,6 +521,15 @@ class TCSCDevice:
         """Small-M kernel: 0 = automatic (default), 1 = never, 2 = every call,
         3 = every call without the producer/consumer walk (M <= 4)."""
         _check(lib().tcsc_hip_set_small_m(self._h, mode), "tcsc_hip_set_small_m")
+
+    def set_host_chunks(self, chunks: int) -> None:
+        """Host-pointer calls: 0 = automatic M-chunk pipeline (default), n =
+        force n chunks (1 = one H2D / compute / D2H, no overlap)."""
+        _check(lib().tcsc_hip_set_host_chunks(self._h, chunks), "tcsc_hip_set_host_chunks")
+
+    def host_chunk_rows(self, M: int) -> int:
+        """Rows per chunk of a host-pointer call with M rows (M = unchunked)."""
+        return int(lib().tcsc_hip_host_chunk_rows(self._h, M))
 
     def call_kernel(self, M: int) -> str:
         """Device kernel a call with M rows launches."""

@@ -113,6 +113,33 @@ def test_threads_host_pointer_calls(tsg, oracle_mod):
     h.close()
 
 
+@pytest.mark.parametrize("chunks", [3, 5, 16])
+def test_host_pointer_pipeline_chunks(tsg, oracle_mod, chunks):
+    """The host-pointer call pipelined by M chunks (H2D / compute / D2H on three
+    streams + a helper thread) with M not divisible by the chunk: comp_func and
+    the PReLU twin stay bit-exact, and the handle can switch back to one
+    unchunked call."""
+    O = oracle_mod
+    K, N, M = 800, 1300, 1000
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 26))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.set_host_chunks(chunks)
+    rows = h.host_chunk_rows(M)
+    assert rows % 128 == 0 and rows < M and M % rows != 0
+    X = O.init_x_frac(M, K, 27)
+    bn = np.linspace(-3, 3, N).astype(np.float32)
+    al = np.linspace(0.1, 0.5, N).astype(np.float32)
+    for _ in range(2):
+        Y = h.gemm(X, bn)
+        assert np.array_equal(Y.view(np.uint32), O.base_tcsc(X, t, bn).view(np.uint32))
+    Yp = h.gemm_prelu(X, bn, al)
+    assert np.array_equal(Yp.view(np.uint32), O.base_tcsc_prelu(X, t, bn, al).view(np.uint32))
+    h.set_host_chunks(1)
+    assert h.host_chunk_rows(M) == M
+    assert np.array_equal(h.gemm(X, bn).view(np.uint32), Y.view(np.uint32))
+    h.close()
+
+
 @pytest.mark.parametrize("M", [4096, 96])
 def test_graph_capture_after_reserve(tsg, oracle_mod, M):
     """tcsc_hip_reserve(max_M) prepares every width a call with M <= max_M runs;
@@ -145,6 +172,47 @@ def test_graph_capture_after_reserve(tsg, oracle_mod, M):
         rows = np.r_[0:16, M - 16:M]
         ref = O.base_tcsc(np.ascontiguousarray(Xn[rows]), t, bn)
         assert np.array_equal(_bits(Ys)[rows], ref.view(np.uint32)), seed
+    h.close()
+
+
+def test_capture_keeps_uncaptured_ordering(tsg, oracle_mod):
+    """An uncaptured call A on s3 is still reading the shared X^T buffer when a
+    call is captured on s1; a later uncaptured call C on s2 must still wait
+    for A before its staging overwrites X^T (the capture does not reset what
+    uncaptured calls wait for).  A's and C's results stay bit-exact."""
+    import torch
+    O = oracle_mod
+    K, N, M = 4096, 8192, 4096
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 25))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    h.reserve(M)
+    bn = np.linspace(-1, 1, N).astype(np.float32)
+    b = torch.from_numpy(bn).cuda()
+    XAn, XCn = O.init_x_frac(M, K, 5), O.init_x_frac(M, K, 6)
+    XA, XC = torch.from_numpy(XAn).cuda(), torch.from_numpy(XCn).cuda()
+    Xg, Yg = torch.zeros((M, K), device="cuda"), torch.empty((M, N), device="cuda")
+    YA, YC = torch.empty((M, N), device="cuda"), torch.empty((M, N), device="cuda")
+    s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s1):  # warm-up outside capture
+        h.gemm_torch(Xg, b, Yg)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s3):
+        h.gemm_torch(XA, b, YA)          # A: uncaptured, still running below
+    with torch.cuda.stream(s1):
+        g.capture_begin()                # (no device sync, unlike torch.cuda.graph)
+        h.gemm_torch(Xg, b, Yg)
+        g.capture_end()
+    with torch.cuda.stream(s2):
+        h.gemm_torch(XC, b, YC)          # C: must wait for A's kernel
+    torch.cuda.synchronize()
+    rows = np.r_[0:32, M // 2:M // 2 + 32, M - 32:M]
+    for X, Y in ((XAn, YA), (XCn, YC)):
+        ref = O.base_tcsc(np.ascontiguousarray(X[rows]), t, bn)
+        assert np.array_equal(_bits(Y)[rows], ref.view(np.uint32))
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(Yg, torch.zeros_like(Yg) + b)
     h.close()
 
 
