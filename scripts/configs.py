@@ -33,11 +33,17 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--all-widths", action="store_true")
     ap.add_argument("--only", default="", help="substring filter on shape names")
+    ap.add_argument("--shape", action="append", default=[],
+                    help="extra shape M,K,N,s (repeatable); with --shape only these run unless --only is given")
     a = ap.parse_args()
+    shapes = list(SHAPES)
+    if a.shape:
+        extra = [("shape %s" % sh, *map(int, sh.split(","))) for sh in a.shape]
+        shapes = extra + (shapes if a.only else [])
     import torch
     import oracle as O
     dev = torch.device("cuda", 0)
-    for name, M, K, N, s in SHAPES:
+    for name, M, K, N, s in shapes:
       if a.only and a.only not in name:
           continue
       for width in ([0, 64, 32, 16, 8] if a.all_widths else [0]):

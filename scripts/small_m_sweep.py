@@ -47,10 +47,15 @@ for M in (int(v) for v in a.M.split(",")):
         ms /= max(n, 1)
         Ys[name] = Y
         adds = M * (nnz + a.N)
+        # bytes the launch moves at least: its device image once, X once, Y once
+        img = h.call_image_bytes(M)
+        moved = img + 4 * (M * a.K + M * a.N + a.N)
         out[name] = {"kernel_ms": round(ms, 5), "Tadds": round(adds / ms / 1e9, 3),
                      "valu_frac": round(adds / ms / 1e9 / 78.64, 4),
                      "tcsc_GBps": round(tcsc_bytes / ms / 1e6, 1),
-                     "hbm_frac_on_tcsc_bytes": round(tcsc_bytes / ms / 1e6 / 8000.0, 4)}
+                     "hbm_frac_on_tcsc_bytes": round(tcsc_bytes / ms / 1e6 / 8000.0, 4),
+                     "image_bytes": img, "bytes_moved_min": moved,
+                     "hbm_frac_on_bytes_moved": round(moved / ms / 1e6 / 8000.0, 4)}
     out["bit_identical"] = bool(torch.equal(Ys["ell"].view(torch.int32), Ys["jit"].view(torch.int32)))
     h.set_small_m(0)
     out["auto"] = h.call_kernel(M)

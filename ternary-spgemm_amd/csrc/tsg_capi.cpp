@@ -1064,6 +1064,18 @@ extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)
     return h->kind == tsg_tcsc::kJit ? "tsg_jit_kernel" : "tsg_tcsc_rx_kernel";
 }
 
+extern "C" int64_t tcsc_hip_call_image_bytes(tsg_tcsc *h, int M)
+{
+    if (!h || M <= 0) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int ev = pick_ell_variant(h, M);
+    if (ev >= 0) return h->ell[ev].ready ? h->ell[ev].bytes : 0;
+    if (h->kind != tsg_tcsc::kJit) return (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
+    const JitShape sh = pick_jit_shape(h, M);
+    const tsg_tcsc::JitVariant &v = h->jv[shape_index(sh.nw, sh.waves)];
+    return v.mod.function ? v.code_bytes + v.wcode_words * 4 : 0;
+}
+
 extern "C" int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K)
 {
     return run_host(h, X, b, nullptr, Y, M, N, K, false);

@@ -89,7 +89,11 @@ constexpr int kJitXRegs = 96;                           // X slot registers v[8 
 constexpr int kJitSlotRegs = 4;                         // one X slot = one k-row pair (2 x 2 M rows)
 constexpr int kJitSlots = kJitXRegs / kJitSlotRegs;     // 24 X slots
 constexpr uint32_t kJitMagic0 = 0x7453474a, kJitMagic1 = 0x314a4954;
-constexpr uint32_t kJitFormat = 2;                      // region header word 7 bits 8+: k-pair layout
+constexpr uint32_t kJitFormat = 2;                      // region header word 7 bits 8-15: k-pair layout
+// region header word 7 bit 16: the DMA pieces take their in-group offset from
+// the instruction offset field (one M0 per 4 pieces); the dispatcher then
+// subtracts (piece & 3) KiB from its per-piece global offsets
+constexpr uint32_t kJitM0kFlag = 1u << 16;
 
 // Stream width: columns per generated stream.  kJitNW (64) is the default;
 // narrower streams (32, 16, 8: same register contract, fewer accumulators,

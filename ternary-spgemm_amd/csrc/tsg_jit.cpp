@@ -16,6 +16,7 @@
 #include <elf.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -76,11 +77,13 @@ struct Emit {
         c.push_back(0xd9fe0000u | off);
         c.push_back((d << 24) | a);
     }
-    // global_load_lds_dwordx4 v[voff], s[84:85]   (LDS-DMA, destination M0)
-    void glds_x4(uint32_t voff)
+    // global_load_lds_dwordx4 v[voff], s[84:85] offset:off   (LDS-DMA: global
+    // s[84:85] + v[voff] + off -> LDS M0 + off; the offset applies to BOTH
+    // addresses on gfx950, scripts/glds_offset_micro.hip)
+    void glds_x4(uint32_t voff, uint32_t off = 0)
     {
         align8();
-        c.push_back(0xddf48000u);
+        c.push_back(0xddf48000u | (off & 0xfffu));
         c.push_back((84u << 16) | voff);
     }
     // global_load_dword v[sink], v[lane*128], s[88:89]   (code prefetch into L2)
@@ -218,6 +221,17 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     const int nch = img.nch, ntiles = img.Npad / tile_cols;
     const std::vector<StepSpec> plan = plan_steps(K, N, B, nch, nw);
     const int steps = (int)plan.size();
+    // LDS-DMA issue (TSG_JIT_DMA="spread,m0k" overrides, A/B): the pieces that
+    // stage step q + kJitRing - 1 go out spread over the first `spread` of step
+    // q's read groups instead of all at the step start (every wave of a CU
+    // reaches the step start together after the barrier: issued at once, the
+    // pieces queue at the CU's vector-memory path and stall every wave);
+    // m0k: one M0 write per 4 pieces, the piece offset in the instruction's
+    // offset field (the dispatcher subtracts it from the per-piece global
+    // offsets; region header word 7, kJitM0kFlag)
+    double dma_spread = 0.5;
+    int m0k = 1;
+    if (const char *dv = std::getenv("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d", &dma_spread, &m0k);
     // X slots: all of v[8 : 104) for BaseTCSC; BlockedTCSC keeps y of half the
     // columns (nw registers) at the top of that range
     const int S = B ? (kJitXRegs - nw) / kJitSlotRegs : kJitSlots;
@@ -235,7 +249,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)waves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
-                             (uint32_t)kJitRing | kJitFormat << 8});
+                             (uint32_t)kJitRing | kJitFormat << 8 | (uint32_t)(m0k ? kJitM0kFlag : 0u)});
     Emit E{code, std::getenv("TSG_JIT_NOALIGN") == nullptr};
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
@@ -287,10 +301,11 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         }
     };
     int base_chunk = -1;  // chunk whose base s[84:85] holds
-    // stage step q's chunk into LDS buffer q % kJitRing; M0 = s83 (this wave's first
-    // piece, set by the dispatcher) + buffer + piece offset
-    auto emit_dma = [&](int q) {
-        if (d_nodma) return;
+    // stage step q's chunk into LDS buffer q % kJitRing: the chunk base, then
+    // pieces 0..kPieces-1 (dma_piece); M0 = s83 (this wave's first piece, set
+    // by the dispatcher) + buffer + piece offset (m0k: the first of 4 pieces'
+    // offset, the others by the instruction offset)
+    auto dma_begin = [&](int q) {
         const int j = plan[(size_t)q].chunk;
         if (j == 0 || base_chunk < 0 || j < base_chunk) {
             E.base_reset();
@@ -300,11 +315,19 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         }
         base_chunk = j;
         E.nop(4);  // SALU-written SGPR base -> VMEM
-        for (int i = 0; i < kPieces; i++) {
+    };
+    auto dma_piece = [&](int q, int i) {
+        const uint32_t sub = m0k ? (uint32_t)(i & 3) : 0u;
+        if (sub == 0) {
             E.m0_wave((uint32_t)(q % kJitRing) * kBufBytes + (uint32_t)i * kPairBytes);
             E.nop(0);  // M0 -> LDS-DMA
-            E.glds_x4(kDmaOffV + (uint32_t)i);
         }
+        E.glds_x4(kDmaOffV + (uint32_t)i, sub * kPairBytes);
+    };
+    auto emit_dma = [&](int q) {  // prologue: every piece at once
+        if (d_nodma) return;
+        dma_begin(q);
+        for (int i = 0; i < kPieces; i++) dma_piece(q, i);
     };
 
     // X read schedule.  The wave's reads (k-row pairs with an entry), over all
@@ -393,23 +416,43 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         live[col] = 1;
                     }
                 };
-                if (q + kJitRing - 1 < steps) emit_dma(q + kJitRing - 1);
-                // code touches go out AFTER the step's DMA: VMEM loads return in
-                // order, so the step's closing vmcnt(ntouch) waits for every DMA
-                // piece but lets the touches (L2 misses) run into the next step
-                for (uint32_t d = 0; d < ntouch; d++) {
-                    E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
-                    E.nop(4);
-                    E.code_touch(kSinkV, kLane128V);
-                }
+                // code touches go out AFTER the step's last DMA piece: VMEM loads
+                // return in order, so the step's closing vmcnt(ntouch) waits for
+                // every DMA piece but lets the touches (L2 misses) run into the
+                // next step
+                auto touches = [&] {
+                    for (uint32_t d = 0; d < ntouch; d++) {
+                        E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
+                        E.nop(4);
+                        E.code_touch(kSinkV, kLane128V);
+                    }
+                };
                 const Section &sec = secs[q];
                 const int nrd = (int)sec.reads.size();
-                for (int i0 = 0; i0 < nrd; i0 += G) {
+                const int ngroups = (nrd + G - 1) / G;
+                const int qd = q + kJitRing - 1;  // the step whose chunk this step stages
+                const bool dma = qd < steps && !d_nodma;
+                // pieces go out before read groups 0 .. span-1 (span 0: all at the step start)
+                const int span = dma ? std::min(ngroups, (int)std::ceil(dma_spread * ngroups)) : 0;
+                int pieces_out = 0;
+                auto pieces_upto = [&](int upto) {
+                    for (; pieces_out < upto; pieces_out++) dma_piece(qd, pieces_out);
+                    if (pieces_out == kPieces && upto == kPieces) touches();
+                };
+                if (dma) {
+                    dma_begin(qd);
+                    if (span == 0) pieces_upto(kPieces);
+                } else {
+                    touches();
+                }
+                for (int i0 = 0, grp = 0; i0 < nrd; i0 += G, grp++) {
                     const int i1 = std::min(nrd, i0 + G);
                     const int64_t g1 = first[q] + i1;
                     issue_reads(g1, q);  // (only if the schedule left the group unread)
                     wait_reads(g1);
                     issue_reads(g1 + RA, q + 1);
+                    if (dma && grp < span && pieces_out < kPieces)  // this group's share of the pieces
+                        pieces_upto(std::min(kPieces, ((grp + 1) * kPieces + span - 1) / span));
                     // per column its entries of the group (ascending k); columns in pairs, interleaved
                     std::vector<std::vector<uint32_t>> xs(nw);
                     for (int i = i0; i < i1; i++) {
@@ -429,6 +472,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                             E.pk_acc(kAcc0 + 2u * (uint32_t)col, kTmp0 + 2u * (uint32_t)(col - sp.c0));
                             live[col] = 0;
                         }
+                if (dma && pieces_out < kPieces) pieces_upto(kPieces);
                 issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
                 E.wait_vm(ntouch);
                 if (!d_nobar) E.barrier();

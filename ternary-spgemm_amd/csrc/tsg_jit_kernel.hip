@@ -68,6 +68,7 @@ constexpr int kJChunk = 96;                          // K rows per chunk = 48 k-
 constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB
 constexpr int kJPieces = kJChunk / 2 / kJWaves;      // LDS-DMA pieces (1-KiB pair rows) per wave per chunk
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
+constexpr uint32_t kJM0kFlag = 1u << 16;  // header word 7: piece offsets in the DMA instruction (tsg_internal.h)
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 typedef float F32x16 __attribute__((ext_vector_type(16)));
@@ -157,12 +158,16 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + stream]);
     const uint32_t lb0 = (uint32_t)lane * 16u, lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
     // LDS-DMA piece i of this wave = pair row pr = wave * P + i of the chunk: the
-    // lane's 16 B at ((pr * Mp/2) + m0/2 + lane) * 16 from the chunk base
+    // lane's 16 B at ((pr * Mp/2) + m0/2 + lane) * 16 from the chunk base.  With
+    // the header's m0k flag the generated code adds (i & 3) KiB through the
+    // instruction offset (to the LDS and the global address alike): subtracted
+    // here (never negative: pr >= i and a pair row of X^T is >= 1 KiB)
+    const uint32_t m0k = (hdr[7] & kJM0kFlag) ? 1u : 0u;
     uint32_t off[kJPieces];
 #pragma unroll
     for (int i = 0; i < kJPieces; i++) {
         const uint32_t pr = (uint32_t)(wave * kJPieces + i);
-        off[i] = (pr * ((uint32_t)Mp / 2u) + (uint32_t)m0 / 2u + (uint32_t)lane) * 16u;
+        off[i] = (pr * ((uint32_t)Mp / 2u) + (uint32_t)m0 / 2u + (uint32_t)lane) * 16u - m0k * (uint32_t)(i & 3) * 1024u;
     }
     const uint32_t wb = (uint32_t)(wave * kJPieces) * 1024u;  // s83
     const uint32_t l128 = (uint32_t)lane * 128u;

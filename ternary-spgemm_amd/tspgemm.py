@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_create_blocked", "tsg_jit_codegen_blocked", "tsg_blocked_tcsc_validate",
     "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tcsc_hip_jit_waves", "tsg_jit_codegen_w", "tsg_jit_codegen_wv",
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
-    "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows",
+    "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
 )
 
 
@@ -127,6 +127,7 @@ def lib() -> C.CDLL:
     L.tcsc_hip_set_small_m.argtypes = [H, C.c_int]
     L.tcsc_hip_set_host_chunks.argtypes = [H, C.c_int]
     L.tcsc_hip_host_chunk_rows.argtypes = [H, C.c_int]
+    L.tcsc_hip_call_image_bytes.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.restype = C.c_char_p
     L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
@@ -136,8 +137,10 @@ def lib() -> C.CDLL:
     L.tcsc_hip_jit_waves.argtypes = [H, C.c_int]
     L.tcsc_hip_set_jit_width.argtypes = [H, C.c_int]
     for f in EXPORTED_SYMBOLS:
-        if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name", "tcsc_hip_call_kernel"):
+        if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name", "tcsc_hip_call_kernel",
+                     "tcsc_hip_call_image_bytes"):
             getattr(L, f).restype = C.c_int
+    L.tcsc_hip_call_image_bytes.restype = C.c_int64
     _LIB = L
     return L
 
@@ -530,6 +533,11 @@ class TCSCDevice:
     def host_chunk_rows(self, M: int) -> int:
         """Rows per chunk of a host-pointer call with M rows (M = unchunked)."""
         return int(lib().tcsc_hip_host_chunk_rows(self._h, M))
+
+    def call_image_bytes(self, M: int) -> int:
+        """Device image bytes a call with M rows reads (ELL image or generated
+        code; 0 if not built yet)."""
+        return int(lib().tcsc_hip_call_image_bytes(self._h, M))
 
     def call_kernel(self, M: int) -> str:
         """Device kernel a call with M rows launches."""

@@ -34,7 +34,11 @@ class Geom:
         assert self.streams == self.waves and self.msplit == 1 and self.tile_m == 128
         self.tile_cols = self.streams * self.nw
         self.ring = int(code[7]) & 0xFF
-        assert int(code[7]) >> 8 == 2, "region must use the k-pair X^T layout (format 2)"
+        assert (int(code[7]) >> 8) & 0xFF == 2, "region must use the k-pair X^T layout (format 2)"
+        # DMA pieces take their in-group offset from the instruction offset (one
+        # M0 per 4 pieces; the dispatcher subtracts it from the global offsets)
+        self.m0k = (int(code[7]) >> 16) & 1
+        assert int(code[7]) >> 17 == 0
         self.pairs = self.chunk // 2                  # k-row pairs per chunk
         self.pair_bytes = self.tile_m * 8             # one pair row of the tile in LDS: 1 KiB
         self.buf_bytes = self.pairs * self.pair_bytes
@@ -115,9 +119,9 @@ def _decode(code, pc, G):
     if w0 == 0xDC508000:
         assert w1 == (G.sink_v << 24) | (88 << 16) | G.l128_v
         return "touch", (), 2
-    if w0 == 0xDDF48000:
+    if (w0 & 0xFFFFF000) == 0xDDF48000:  # global_load_lds_dwordx4 v, s[84:85] offset:(w0 & 0xFFF)
         assert (w1 >> 16) == 84
-        return "glds", (w1 & 0xFF,), 2
+        return "glds", (w1 & 0xFF, w0 & 0xFFF), 2
     if (w0 & 0xFFFFFC00) == 0xD3B24000:  # v_pk_add_f32
         kind, f = _classify_pk(w0, w1, G)
         return kind, f, 2
@@ -183,14 +187,18 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     assert wv.touch is not None and wv.touch + 63 * 128 + 4 <= region_bytes, "prefetch past region"
                     wv.pending.append([])
                 elif kind == "glds":
-                    i = f[0] - G.dma_v
+                    i, off = f[0] - G.dma_v, f[1]
                     assert 0 <= i < PIECES
+                    # the dispatcher's off[i] minus the instruction offset it
+                    # expects (m0k: (i & 3) KiB): the global side reads pair row pr
+                    assert off == ((i & 3) * PAIR_BYTES if G.m0k else 0), "DMA offset disagrees with the dispatcher"
                     pr = wv.w * PIECES + i  # the pair row this lane set copies (dispatcher off[i])
                     j, rem = divmod(wv.base - XT_BASE, stride)
                     assert rem == 0 and 0 <= j < nch
-                    assert wv.m0 % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
+                    dst = wv.m0 + off  # the offset applies to the LDS address too
+                    assert dst % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
                     data = XP[j * PAIRS + pr, m0 // 2:m0 // 2 + 64].reshape(-1).copy()
-                    wv.pending.append([(wv.m0, data, phase)])
+                    wv.pending.append([(dst, data, phase)])
                 elif kind == "wait_vm":  # loads return in order: all but the newest f[0] land
                     n_land = max(len(wv.pending) - f[0], 0)
                     for op in wv.pending[:n_land]:
