@@ -102,7 +102,7 @@ void tcsc_hip_destroy(tsg_tcsc *h);
  * result is the unchunked one bit for bit (rows are independent). */
 int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, int N, int K);
 
-/* Host-pointer pipeline chunks: 0 = automatic (one per ~32 MiB of Y, at most
+/* Host-pointer pipeline chunks: 0 = automatic (one per ~16 MiB of Y, at most
  * 16, >= 256 rows, multiples of 128; small-M calls whole), or force n chunks
  * (1 = no pipeline; tests and A/B).  tcsc_hip_host_chunk_rows: rows per chunk
  * a call with M rows uses (M = unchunked).  Extension: no reference

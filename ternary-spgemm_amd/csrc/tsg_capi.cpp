@@ -265,20 +265,34 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 }
 
 // Tile map groups (tsg_jit_map.h) per call: gn column tiles x gm M tiles per
-// XCD group.  2 x 16 keeps the CU pairs that share an instruction cache on one
-// code stream (configs[2]: 1.24-1.25 ms vs 1.26-1.28 at 4 x 8; (64000, 16384,
-// 4096): 27.0 vs 28.0-28.7 ms); with at most 4 column tiles or 8 M tiles,
-// 4 x 8 (every column tile, or every M tile, of the XCD's group shares its
-// X^T chunks or code): (16000, 8192, 2048) 1.19-1.21 vs 1.31-1.34 ms,
-// (1024, 4096, 16384) 0.311-0.313 vs 0.319-0.323 ms
-// (profiles/r02_jit_map_bench_ab.txt).  TSG_JIT_GN / TSG_JIT_GM override (A/B).
-void pick_jit_map(int mtiles, int ntiles, int &gn, int &gm)
+// XCD group, 32 workgroups (the XCD's CUs).  Measured
+// (profiles/r03_map_density_ab.txt, r02_jit_map_bench_ab.txt):
+//  * with at most 4 column tiles or 8 M tiles, 4 x 8: every column tile, or
+//    every M tile, of the XCD's group shares its X^T chunks or code
+//    ((16000, 8192, 2048) 1.19-1.21 vs 1.31-1.34 ms at 2 x 16);
+//  * sparse W (density <= 3/16, s >= 8): 4 x 8 -- a column tile's code is
+//    short, so sharing each X^T slab between more column tiles wins (s = 16:
+//    0.565 vs 0.604 ms at 2 x 16; s = 8: 0.769 vs 0.792);
+//  * long streams (K >= 8192): 1 x 32, every CU of the XCD on one column
+//    tile's code ((64000, 16384, 4096): 25.6 vs 26.8 ms);
+//  * otherwise 2 x 16: the CU pairs that share an instruction cache on one
+//    code stream (configs[2] 1.212 ms vs 1.264 at 4 x 8; s = 2 2.554 vs 2.712).
+// TSG_JIT_GN / TSG_JIT_GM override (A/B).
+void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm)
 {
     static const int env_gn = [] { const char *e = getenv("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
     static const int env_gm = [] { const char *e = getenv("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
-    const bool small = ntiles <= 4 || mtiles <= 8;
-    gn = std::min(env_gn > 0 ? env_gn : small ? 4 : 2, std::max(ntiles, 1));  // a group never exceeds the grid
-    gm = std::min(env_gm > 0 ? env_gm : small ? 8 : 16, std::max(mtiles, 1));
+    const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
+    int n = 2, m = 16;
+    if (ntiles <= 4 || mtiles <= 8 || density <= 0.1875) {
+        n = 4;
+        m = 8;
+    } else if (h->K >= 8192) {
+        n = 1;
+        m = 32;
+    }
+    gn = std::min(env_gn > 0 ? env_gn : n, std::max(ntiles, 1));  // a group never exceeds the grid
+    gm = std::min(env_gm > 0 ? env_gm : m, std::max(mtiles, 1));
 }
 
 int handle_stream(tsg_tcsc *h, hipStream_t &s)
@@ -555,7 +569,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         HIP_TRY(hipEventRecord(h->ev0[slot], s));
     }
     int gn = 2, gm = 16;
-    if (h->kind == tsg_tcsc::kJit) pick_jit_map(Mp / tsg::kJitTileM, jv->Npad / (jv->nw * jv->waves), gn, gm);
+    if (h->kind == tsg_tcsc::kJit) pick_jit_map(h, Mp / tsg::kJitTileM, jv->Npad / (jv->nw * jv->waves), gn, gm);
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves, jv->waves, gn, gm, s)
@@ -580,14 +594,16 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     return TSG_OK;
 }
 
-// Chunks of the host-pointer pipeline: one per ~32 MiB of Y (the PCIe leg
+// Chunks of the host-pointer pipeline: one per ~16 MiB of Y (the PCIe leg
 // that binds: Y is the largest transfer), at most kHostChunksMax, each a whole
 // number of 128-row M tiles and at least 256 rows; calls the small-M kernel
-// takes run whole.  configs[2] (268 MB of Y): 8 chunks of 512 rows.
+// takes run whole.  configs[2] (268 MB of Y): 16 chunks of 256 rows, 5.45 ms
+// per call (8 chunks 5.50, 4 chunks 5.72, unchunked 7.38;
+// profiles/r03b_host_pipe_ab.jsonl).
 int host_chunk_rows(const tsg_tcsc *h, int M)
 {
     const int64_t ybytes = (int64_t)M * h->N * 4;
-    int n = h->host_chunks > 0 ? h->host_chunks : (int)std::min<int64_t>(ybytes >> 25, tsg_tcsc::kHostChunksMax);
+    int n = h->host_chunks > 0 ? h->host_chunks : (int)std::min<int64_t>(ybytes >> 24, tsg_tcsc::kHostChunksMax);
     n = std::min(n, tsg_tcsc::kHostChunksMax);
     if (n <= 1 || (h->host_chunks <= 0 && pick_ell_variant(h, M) >= 0)) return M;
     int rows = (M + n - 1) / n;
