@@ -229,9 +229,15 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // m0k: one M0 write per 4 pieces, the piece offset in the instruction's
     // offset field (the dispatcher subtracts it from the per-piece global
     // offsets; region header word 7, kJitM0kFlag)
+    // lag: 1 = a step's pieces are waited for at the end of that step, so the
+    // next step's first reads can go out before the barrier (read-ahead
+    // across steps); 2 = they are waited for one step later (the DMA gets
+    // two steps to land -- for X^T served from far memory) and each step's
+    // reads start after its barrier
     double dma_spread = 0.5;
-    int m0k = 1;
-    if (const char *dv = std::getenv("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d", &dma_spread, &m0k);
+    int m0k = 1, lag = 1;
+    if (const char *dv = std::getenv("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d,%d", &dma_spread, &m0k, &lag);
+    if (lag != 2) lag = 1;
     // X slots: all of v[8 : 104) for BaseTCSC; BlockedTCSC keeps y of half the
     // columns (nw registers) at the top of that range
     const int S = B ? (kJitXRegs - nw) / kJitSlotRegs : kJitSlots;
@@ -316,6 +322,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         base_chunk = j;
         E.nop(4);  // SALU-written SGPR base -> VMEM
     };
+    int vm_step = 0;  // VMEM operations (DMA pieces, code touches) issued in the current step
     auto dma_piece = [&](int q, int i) {
         const uint32_t sub = m0k ? (uint32_t)(i & 3) : 0u;
         if (sub == 0) {
@@ -323,6 +330,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             E.nop(0);  // M0 -> LDS-DMA
         }
         E.glds_x4(kDmaOffV + (uint32_t)i, sub * kPairBytes);
+        vm_step++;
     };
     auto emit_dma = [&](int q) {  // prologue: every piece at once
         if (d_nodma) return;
@@ -425,8 +433,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
                         E.nop(4);
                         E.code_touch(kSinkV, kLane128V);
+                        vm_step++;
                     }
                 };
+                vm_step = 0;
                 const Section &sec = secs[q];
                 const int nrd = (int)sec.reads.size();
                 const int ngroups = (nrd + G - 1) / G;
@@ -450,7 +460,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     const int64_t g1 = first[q] + i1;
                     issue_reads(g1, q);  // (only if the schedule left the group unread)
                     wait_reads(g1);
-                    issue_reads(g1 + RA, q + 1);
+                    issue_reads(g1 + RA, lag == 2 ? q : q + 1);
                     if (dma && grp < span && pieces_out < kPieces)  // this group's share of the pieces
                         pieces_upto(std::min(kPieces, ((grp + 1) * kPieces + span - 1) / span));
                     // per column its entries of the group (ascending k); columns in pairs, interleaved
@@ -473,8 +483,14 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                             live[col] = 0;
                         }
                 if (dma && pieces_out < kPieces) pieces_upto(kPieces);
-                issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
-                E.wait_vm(ntouch);
+                if (lag == 1) {
+                    issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
+                    E.wait_vm(ntouch);  // this step's pieces (the touches may run on)
+                } else {
+                    // the previous step's pieces: only its touches and this
+                    // step's operations may still be in flight
+                    E.wait_vm(ntouch + (uint32_t)vm_step);
+                }
                 if (!d_nobar) E.barrier();
             }
             E.wait_vm0();  // no load outstanding past the stream
