@@ -101,7 +101,7 @@ namespace {
 // pick_ell_variant), the variant with 8-row tiles, and the M up to which
 // 8-row tiles are used.
 constexpr int kEllAutoMaxM = 64;
-constexpr int kEllAutoMaxMChunked = 16;
+constexpr int kEllAutoMaxMChunked = 32;
 constexpr int kEllTile8 = 2;
 constexpr int kEllMidM = 32;
 constexpr int64_t kEllPcRowsMaxMN = 32768;
@@ -411,7 +411,8 @@ bool use_ell_pc(const tsg_tcsc *h, int v) { return v == 0 && ell_pc_available(h)
 // an 8-row chunk of K = 4096 fits LDS, one stream per column); above that the
 // largest tile whose chunk holds K.  Automatic up to M = 64 when an 8-row
 // tile holds K in one chunk (ELL 98 us vs jit 123 us at M = 64, K = 4096),
-// else up to M = 16 (K = 16384: 0.22 vs 0.55 ms); and up to M = 1024 while the
+// else up to M = 32 (K = N = 16384: M = 16 0.18 vs 0.39 ms, M = 32 0.29 vs 0.39 ms,
+// M = 40 0.51 vs 0.39 ms; profiles/r03_half_tile_ab.txt); and up to M = 1024 while the
 // jit kernel would have at most 64 workgroups (the reference's (1000, 2048,
 // 512): 31 vs 52 us; (256, 4096, 1024): 34 vs 91 us; at 128 workgroups the
 // jit kernel wins: (1024, 1024, 1024) 32 vs 35 us;
@@ -424,7 +425,11 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     const int64_t jit_wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                             ((h->N + 8 * tsg::kJitWaves - 1) / (8 * tsg::kJitWaves));
     const bool starved = M <= kEllStarvedMaxM && jit_wgs <= kEllStarvedWgs;
-    if (h->small_m < 2 && M > (one8 ? kEllAutoMaxM : kEllAutoMaxMChunked) && !starved) return -1;
+    static const int auto_max = [] {  // TSG_ELL_MAXM: A/B of the small-M boundary
+        const char *e = getenv("TSG_ELL_MAXM");
+        return e ? atoi(e) : kEllAutoMaxM;
+    }();
+    if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) && !starved) return -1;
     int v = 0;
     if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
         v = kEllTile8;

@@ -234,7 +234,18 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // across steps); 2 = they are waited for one step later (the DMA gets
     // two steps to land -- for X^T served from far memory) and each step's
     // reads start after its barrier
-    double dma_spread = 0.5;
+    //
+    // Default spread (profiles/r03_dma_lag_ab.txt, r03c_dma_spread_far_ab.txt):
+    // 0 -- every piece at the step start -- for long sparse streams (K >= 8192,
+    // density <= 3/16: short steps over X^T from far memory, where a late
+    // piece does not land in time: (64000, 16384, 4096) s = 8 15.7 -> 12.6 ms,
+    // (16000, 8192, 2048) s = 8 0.92 -> 0.74 ms); else 0.5 (configs[2] 1.229
+    // -> 1.197 ms, configs[1] 0.101 -> 0.096 ms, (64000, 16384, 4096) s = 4
+    // 26.4 -> 25.2 ms).  Lag 2 gained nowhere (kept as an A/B option).
+    const int64_t nnz_all = B ? (int64_t)csp[(int64_t)(K / B) * N] + csn[(int64_t)(K / B) * N]
+                              : (int64_t)csp[N] + csn[N];
+    const double density = (double)nnz_all / std::max(1.0, (double)K * (double)N);
+    double dma_spread = K >= 8192 && density <= 0.1875 ? 0.0 : 0.5;
     int m0k = 1, lag = 1;
     if (const char *dv = std::getenv("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d,%d", &dma_spread, &m0k, &lag);
     if (lag != 2) lag = 1;
