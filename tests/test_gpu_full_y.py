@@ -1,0 +1,59 @@
+"""Every element of Y at BASELINE's full sizes, on the GPU.
+
+With integer-valued X (the reference's own inputs: initX, sparseUtils.h:6-23,
+U[-512, 512]) and integer b, every partial sum of every chain is an integer
+of magnitude < 2^24, so it is exact in fp32 whatever the order: the BaseTCSC
+chain (comp.h:37-63) and ANY fp32 summation of X @ W + b give the same bits.
+That makes a dense fp32 GEMM on the GPU (torch.matmul of X and the dense
++-1 W) an exact reference for the whole [M, N] result at full size -- the
+same argument the reference's own correctness check rests on (main.cpp:206-227
+compares BaseTCSC against its dense GEMM).  Order for non-integer X is pinned
+by the sampled-row oracle tests (test_gpu_parity.py, test_gpu_sweep.py).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _dense_w(csp, csn, rip, rin, K, N, dev):
+    import torch
+    W = torch.zeros((K, N), dtype=torch.float32, device=dev)
+    cols_p = np.repeat(np.arange(N), np.diff(csp))
+    cols_n = np.repeat(np.arange(N), np.diff(csn))
+    W[torch.from_numpy(rip.astype(np.int64)).to(dev), torch.from_numpy(cols_p).to(dev)] = 1.0
+    W[torch.from_numpy(rin.astype(np.int64)).to(dev), torch.from_numpy(cols_n).to(dev)] = -1.0
+    return W
+
+
+@pytest.mark.parametrize("M,K,N,s", [
+    (512, 4096, 4096, 4),        # configs[1]
+    (4096, 4096, 16384, 4),      # configs[2] (the bench workload)
+    (4096, 4096, 16384, 2),      # configs[3]
+    (4096, 4096, 16384, 8),
+    (4096, 4096, 16384, 16),
+    (1000, 2048, 512, 4),        # reference cases (plots/run_benchmark.py:8-33)
+    (16000, 8192, 2048, 8),
+    (64000, 16384, 4096, 4),     # the reference's largest case
+    (37, 16384, 16384, 4),       # small M, K in several chunks
+])
+def test_full_y_integer_x(tsg, M, K, N, s):
+    import torch
+    dev = torch.device("cuda", 0)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    csp, csn, rip, rin = tsg.gen_tcsc(K, N, s, 42)
+    h = tsg.TCSCDevice(csp, csn, rip, rin, K, N, device=0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(12345)
+    X = torch.randint(-512, 513, (M, K), generator=g, device=dev, dtype=torch.int32).to(torch.float32)
+    b = torch.full((N,), 2.0, device=dev)  # main.cpp:194
+    Y = h.gemm_torch(X, b)
+    kernel = h.call_kernel(M)
+    W = _dense_w(csp, csn, rip, rin, K, N, dev)
+    ref = torch.matmul(X, W) + b
+    del W
+    torch.cuda.synchronize()
+    same = torch.equal(Y.view(torch.int32), ref.view(torch.int32))
+    bad = int((Y.view(torch.int32) != ref.view(torch.int32)).sum()) if not same else 0
+    h.close()
+    assert same, f"{bad} of {M * N} elements differ ({kernel})"
