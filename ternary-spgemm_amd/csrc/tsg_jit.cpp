@@ -80,17 +80,18 @@ struct Emit {
     // global_load_lds_dwordx4 v[voff], s[84:85] offset:off   (LDS-DMA: global
     // s[84:85] + v[voff] + off -> LDS M0 + off; the offset applies to BOTH
     // addresses on gfx950, scripts/glds_offset_micro.hip)
+    uint32_t dma_cp = 0, touch_cp = 0;  // cache-policy bits (sc0 16, nt 17, sc1 25) of the DMA / touch loads
     void glds_x4(uint32_t voff, uint32_t off = 0)
     {
         align8();
-        c.push_back(0xddf48000u | (off & 0xfffu));
+        c.push_back(0xddf48000u | (off & 0xfffu) | dma_cp);
         c.push_back((84u << 16) | voff);
     }
     // global_load_dword v[sink], v[lane*128], s[88:89]   (code prefetch into L2)
     void code_touch(uint32_t sink, uint32_t l128)
     {
         align8();
-        c.push_back(0xdc508000u);
+        c.push_back(0xdc508000u | touch_cp);
         c.push_back((sink << 24) | (88u << 16) | l128);
     }
     void m0_wave(uint32_t v) { align8(); c.push_back(0x807cff53u); c.push_back(v); }  // s_add_u32 m0, s83, v
@@ -268,6 +269,14 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
                              (uint32_t)kJitRing | kJitFormat << 8 | (uint32_t)(m0k ? kJitM0kFlag : 0u)});
     Emit E{code, std::getenv("TSG_JIT_NOALIGN") == nullptr};
+    // TSG_JIT_CP="dma,touch": cache-policy bits of the LDS-DMA pieces and the
+    // code touches (hex; 0x20000 = nt, 0x2000000 = sc1, 0x10000 = sc0; A/B)
+    if (const char *cv = std::getenv("TSG_JIT_CP")) {
+        unsigned a = 0, t = 0;
+        std::sscanf(cv, "%x,%x", &a, &t);
+        E.dma_cp = a & 0x2030000u;
+        E.touch_cp = t & 0x2030000u;
+    }
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
     // prefetch), nolgkm (no LDS waits), noreads (no X reads)

@@ -116,10 +116,11 @@ def _decode(code, pc, G):
         return "m0", (w1,), 2
     if w0 == 0x8058FF5C:
         return "touch_addr", (w1,), 2
-    if w0 == 0xDC508000:
+    CP = 0x2030000  # cache-policy bits (sc0, nt, sc1): any combination
+    if (w0 & ~CP) == 0xDC508000:
         assert w1 == (G.sink_v << 24) | (88 << 16) | G.l128_v
         return "touch", (), 2
-    if (w0 & 0xFFFFF000) == 0xDDF48000:  # global_load_lds_dwordx4 v, s[84:85] offset:(w0 & 0xFFF)
+    if (w0 & ~CP & 0xFFFFF000) == 0xDDF48000:  # global_load_lds_dwordx4 v, s[84:85] offset:(w0 & 0xFFF)
         assert (w1 >> 16) == 84
         return "glds", (w1 & 0xFF, w0 & 0xFFF), 2
     if (w0 & 0xFFFFFC00) == 0xD3B24000:  # v_pk_add_f32
