@@ -709,6 +709,9 @@ int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, fl
         }
         cv.notify_all();
         out.join();
+        // on an error, chunks already enqueued may still read d_x / write d_y:
+        // drain them so the next call's copies cannot overtake them
+        if (code) (void)hipStreamSynchronize(s);
         return code;
     };
     for (int i = 0; i < nchunk; i++) {
