@@ -108,13 +108,22 @@ int tcsc_hip_gemm(tsg_tcsc *h, const float *X, const float *b, float *Y, int M, 
  * a call with M rows uses (M = unchunked).  Extension: no reference
  * counterpart. */
 int tcsc_hip_set_host_chunks(tsg_tcsc *h, int chunks);
+int tcsc_hip_host_chunk_rows(tsg_tcsc *h, int M);
+
+/* Optional page-locking of a host buffer the caller passes to repeated
+ * host-pointer calls (e.g. the X and Y of a benchmark loop, perf.cpp:37-71):
+ * the call's copies then DMA directly instead of through the runtime's
+ * pin-on-the-fly staging.  The buffer must stay allocated until
+ * tcsc_hip_host_unregister.  Unregistered (pageable) buffers keep working.
+ * Extension: no reference counterpart. */
+int tcsc_hip_host_register(void *p, size_t bytes);
+int tcsc_hip_host_unregister(void *p);
 
 /* Bytes of the device image a call with M rows reads: the small-M kernel's
  * sliced-ELL image, or the weight-compiled code (+ stream table) of the width
  * that call runs; 0 if that image is not built yet (tcsc_hip_reserve builds
  * it).  For reporting the bytes a launch moves besides X and Y.  Extension. */
 int64_t tcsc_hip_call_image_bytes(tsg_tcsc *h, int M);
-int tcsc_hip_host_chunk_rows(tsg_tcsc *h, int M);
 
 /* DEVICE pointers (on the handle's device), enqueued on `stream`
  * (a hipStream_t; NULL = legacy default stream); returns without waiting.

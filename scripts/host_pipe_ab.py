@@ -24,7 +24,7 @@ def main():
     b = np.full(N, 2.0, np.float32)
     Yd = h.gemm_torch(torch.from_numpy(X).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
     Y = np.empty((M, N), np.float32)
-    for chunks in (1, 4, 8, 12, 16, 0):
+    def run(tag, chunks):
         h.set_host_chunks(chunks)
         h(X, b, Y, M, N, K)
         ts = []
@@ -32,9 +32,15 @@ def main():
             t0 = time.perf_counter()
             h(X, b, Y, M, N, K)
             ts.append((time.perf_counter() - t0) * 1e3)
-        print(json.dumps({"chunks": chunks or "auto", "chunk_rows": h.host_chunk_rows(M),
+        print(json.dumps({"buffers": tag, "chunks": chunks or "auto", "chunk_rows": h.host_chunk_rows(M),
                           "ms_median": round(float(np.median(ts)), 3), "ms_min": round(min(ts), 3),
                           "bit_identical": bool(np.array_equal(Y.view(np.uint32), Yd.view(np.uint32)))}), flush=True)
+
+    for chunks in (1, 4, 8, 12, 16, 0):
+        run("pageable", chunks)
+    with T.registered_host(X, Y):  # tcsc_hip_host_register: the caller's buffers page-locked once
+        for chunks in (1, 16, 0):
+            run("registered", chunks)
 
 
 if __name__ == "__main__":

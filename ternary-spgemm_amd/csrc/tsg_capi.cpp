@@ -1049,6 +1049,24 @@ extern "C" int tcsc_hip_jit_waves(const tsg_tcsc *h, int M)
     return pick_jit_shape(h, M).waves;
 }
 
+// Opt-in page-locking of a caller's host buffer (X or Y of repeated
+// host-pointer calls): the copies of the pipeline then DMA straight from / to
+// it instead of the runtime's pin-on-the-fly staging.  The caller keeps the
+// buffer alive until tcsc_hip_host_unregister.
+extern "C" int tcsc_hip_host_register(void *p, size_t bytes)
+{
+    if (!p || bytes == 0) return fail(TSG_ERR_ARG, "tcsc_hip_host_register: null pointer or zero size");
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_host_unregister(void *p)
+{
+    if (!p) return fail(TSG_ERR_ARG, "tcsc_hip_host_unregister: null pointer");
+    HIP_TRY(hipHostUnregister(p));
+    return TSG_OK;
+}
+
 extern "C" int tcsc_hip_set_host_chunks(tsg_tcsc *h, int chunks)
 {
     if (!h) return fail(TSG_ERR_ARG, "null handle");

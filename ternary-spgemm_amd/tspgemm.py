@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tcsc_hip_jit_waves", "tsg_jit_codegen_w", "tsg_jit_codegen_wv",
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
+    "tcsc_hip_host_register", "tcsc_hip_host_unregister",
 )
 
 
@@ -128,6 +129,8 @@ def lib() -> C.CDLL:
     L.tcsc_hip_set_host_chunks.argtypes = [H, C.c_int]
     L.tcsc_hip_host_chunk_rows.argtypes = [H, C.c_int]
     L.tcsc_hip_call_image_bytes.argtypes = [H, C.c_int]
+    L.tcsc_hip_host_register.argtypes = [vp, C.c_size_t]
+    L.tcsc_hip_host_unregister.argtypes = [vp]
     L.tcsc_hip_call_kernel.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.restype = C.c_char_p
     L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
@@ -329,6 +332,30 @@ def gen_x(M: int, K: int, seed: int, rng: int = 512) -> np.ndarray:
     X = np.empty((M, K), np.float32)
     _check(lib().tsg_gen_x(M * K, rng, seed, _ptr(X)), "tsg_gen_x")
     return X
+
+
+class registered_host:
+    """Context manager: page-locks numpy arrays for repeated host-pointer
+    calls (tcsc_hip_host_register), unlocks them on exit."""
+
+    def __init__(self, *arrays):
+        self.arrays = [a for a in arrays if a is not None and a.size]
+
+    def __enter__(self):
+        done = []
+        try:
+            for a in self.arrays:
+                _check(lib().tcsc_hip_host_register(a.ctypes.data, a.nbytes), "tcsc_hip_host_register")
+                done.append(a)
+        except Exception:
+            for a in done:
+                lib().tcsc_hip_host_unregister(a.ctypes.data)
+            raise
+        return self
+
+    def __exit__(self, *exc):
+        for a in self.arrays:
+            _check(lib().tcsc_hip_host_unregister(a.ctypes.data), "tcsc_hip_host_unregister")
 
 
 def device_count() -> int:

@@ -140,6 +140,28 @@ def test_host_pointer_pipeline_chunks(tsg, oracle_mod, chunks):
     h.close()
 
 
+def test_host_pointer_registered_buffers(tsg, oracle_mod):
+    """Caller buffers page-locked once (tcsc_hip_host_register) for repeated
+    host-pointer calls: same bits as pageable buffers, pipelined or not."""
+    O = oracle_mod
+    K, N, M = 900, 1100, 700
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, 28))
+    h = tsg.TCSCDevice(*t.arrays, K, N)
+    X = O.init_x_frac(M, K, 29)
+    bn = np.linspace(-1, 1, N).astype(np.float32)
+    Y = np.empty((M, N), np.float32)
+    ref = O.base_tcsc(X, t, bn).view(np.uint32)
+    with tsg.registered_host(X, Y):
+        for chunks in (0, 1, 5):
+            h.set_host_chunks(chunks)
+            Y[:] = np.nan
+            h(X, bn, Y, M, N, K)
+            assert np.array_equal(Y.view(np.uint32), ref)
+    h(X, bn, Y, M, N, K)  # unregistered again
+    assert np.array_equal(Y.view(np.uint32), ref)
+    h.close()
+
+
 @pytest.mark.parametrize("M", [4096, 96])
 def test_graph_capture_after_reserve(tsg, oracle_mod, M):
     """tcsc_hip_reserve(max_M) prepares every width a call with M <= max_M runs;
