@@ -9,6 +9,13 @@ Writes <round>_kernel_stats.csv (rocprofv3 --stats copy), <round>_kernel_trace_t
   (HBM section) prescribes: FETCH_SIZE is KiB and reads 1/2 of a wide (16 B/lane)
   coalesced stream on gfx950 -> read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is
   exact for 16-B-per-lane stores -> write bytes = WRITE_SIZE * 1024.
+Dispatches are grouped by (kernel, grid size): the workload's own launches
+(the largest grid of a kernel) are reported under the kernel's name, smaller
+grids of the same kernel (the host-pointer comp_func pipeline launches M
+chunks, bench.py e2e_host_pointers) under "<kernel> [grid G]", so per-launch
+figures never mix launch sizes.  The kernel-trace dispatches get the same
+split (<round>_kernel_trace_by_grid.json: count and average duration per
+grid).
 """
 import collections
 import csv
@@ -32,6 +39,14 @@ if trace:
             w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
             w.writeheader()
             w.writerows(rows)
+        by = collections.defaultdict(list)
+        for r in rows:
+            by[(r["Kernel_Name"].split("(")[0].replace("void ", "").strip(), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))].append(
+                int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        json.dump({f"{k} [grid {g}]": {"dispatches": len(v), "avg_us": sum(v) / len(v) / 1e3,
+                                        "min_us": min(v) / 1e3, "max_us": max(v) / 1e3}
+                   for (k, g), v in sorted(by.items())},
+                  open(dst + "_kernel_trace_by_grid.json", "w"), indent=1)
 
 # per (pass, kernel, counter): total and dispatches; a counter collected in
 # several passes (GRBM_GUI_ACTIVE) is averaged over them, not summed
@@ -42,9 +57,15 @@ for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")))
         k = r["Kernel_Name"]
         if "tsg" not in k or "probe" in k:
             continue
-        kn = k.split("(")[0].replace("void ", "").strip()
+        kn = (k.split("(")[0].replace("void ", "").strip(), int(r["Grid_Size"]))
         tot[kn][r["Counter_Name"]][f] += float(r["Counter_Value"])
         disp[kn][r["Counter_Name"]][f].add(r["Dispatch_Id"])
+# the workload's launches: the largest grid of each kernel
+biggest = {}
+for name, g in tot:
+    biggest[name] = max(g, biggest.get(name, 0))
+tot = {(name if g == biggest[name] else f"{name} [grid {g}]"): v for (name, g), v in tot.items()}
+disp = {(name if g == biggest[name] else f"{name} [grid {g}]"): v for (name, g), v in disp.items()}
 out = {"workload": f"{M}x{K}x{N}s{s}", "kernel": None, "kernels": {}, "per_launch_hbm_bytes": {}}
 for kn, v in tot.items():
     per = {c: sum(x / max(len(disp[kn][c][f]), 1) for f, x in passes.items()) / len(passes)
@@ -80,7 +101,7 @@ for kn, v in tot.items():
         o["lds_util"] = per["SQ_LDS_IDX_ACTIVE"] / (per["GRBM_GUI_ACTIVE"] / 8 * 256)
     out["kernels"][kn] = o
     main = kn.split("::")[-1].split("<")[0]
-    if "transpose" not in main and "hbm_bytes" in o:  # the TCSC kernel
+    if "transpose" not in main and "[grid" not in kn and "hbm_bytes" in o:  # the TCSC kernel
         out["kernel"] = main
         out["per_launch_hbm_bytes"][out["workload"]] = o["hbm_bytes"]
 json.dump(out, open(dst + "_pmc_summary.json", "w"), indent=1)

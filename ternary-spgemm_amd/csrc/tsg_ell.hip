@@ -115,23 +115,25 @@ __device__ __forceinline__ void ell_add(float (&y)[RPL], const float (&x)[8][RPL
 // branch; the last nmax % D blocks are then already in q and run with an
 // early exit and no loads (a load ahead of an exit branch would be sunk past
 // it by the compiler, exposing one memory latency per group).
-template <int RPL, int D>
+// LA: LDS lookahead in blocks -- the reads of block d + LA go out before the
+// adds of block d (LA + 1 register sets of 8 x RPL values).
+template <int RPL, int D, int LA>
 __device__ __forceinline__ void ell_walk(float (&y)[RPL], uint4 (&q)[D], const uint4 *__restrict__ e0, uint32_t off,
                                          uint32_t n8, uint32_t n8pos, uint32_t nmax, uint32_t base)
 {
+    static_assert(LA >= 1 && LA < D, "lookahead");
+    constexpr int NS = LA + 1;  // register sets
     uint32_t g = 0;
     for (; g + D <= nmax; g += D) {
-        float x0[8][RPL], x1[8][RPL];
-        ell_load<RPL>(x0, q[0], base);
+        float x[NS][8][RPL];
+#pragma unroll
+        for (int a = 0; a < LA; a++) ell_load<RPL>(x[a], q[a], base);
 #pragma unroll
         for (int d = 0; d < D; d++) {
-            if (d + 1 < D) {
-                if (d % 2 == 0) ell_load<RPL>(x1, q[d + 1], base);
-                else ell_load<RPL>(x0, q[d + 1], base);
-            }
-            // the reads of block d + 1 stay ahead of the adds of block d
+            if (d + LA < D) ell_load<RPL>(x[(d + LA) % NS], q[d + LA], base);
+            // the reads of block d + LA stay ahead of the adds of block d
             __builtin_amdgcn_sched_barrier(0);
-            ell_add<RPL>(y, d % 2 == 0 ? x0 : x1, g + d < n8pos ? 1.0f : -1.0f);
+            ell_add<RPL>(y, x[d % NS], g + d < n8pos ? 1.0f : -1.0f);
             __builtin_amdgcn_sched_barrier(0);
             const uint32_t nb = g + D + d;  // refill: D blocks ahead, padding past the end
             q[d] = e0[nb < n8 ? (off + nb) * 16 : 0];
@@ -139,16 +141,14 @@ __device__ __forceinline__ void ell_walk(float (&y)[RPL], uint4 (&q)[D], const u
     }
     const uint32_t rest = nmax - g;  // < D, uniform
     if (rest == 0) return;
-    float x0[8][RPL], x1[8][RPL];
-    ell_load<RPL>(x0, q[0], base);
+    float x[NS][8][RPL];
+#pragma unroll
+    for (int a = 0; a < LA; a++) ell_load<RPL>(x[a], q[a], base);
 #pragma unroll
     for (int d = 0; d < D; d++) {
-        if (d + 1 < D) {
-            if (d % 2 == 0) ell_load<RPL>(x1, q[d + 1], base);
-            else ell_load<RPL>(x0, q[d + 1], base);
-        }
+        if (d + LA < D) ell_load<RPL>(x[(d + LA) % NS], q[d + LA], base);
         __builtin_amdgcn_sched_barrier(0);
-        ell_add<RPL>(y, d % 2 == 0 ? x0 : x1, g + d < n8pos ? 1.0f : -1.0f);
+        ell_add<RPL>(y, x[d % NS], g + d < n8pos ? 1.0f : -1.0f);
         __builtin_amdgcn_sched_barrier(0);
         if ((uint32_t)d + 1 >= rest) return;
     }
@@ -222,7 +222,7 @@ __device__ __forceinline__ void ell_stage(float *xs, const float *__restrict__ X
 
 }  // namespace
 
-template <int LG, int RPL, int WPG, bool PRELU>
+template <int LG, int RPL, int WPG, int LA, bool PRELU>
 __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
     const float *__restrict__ X, const uint4 *__restrict__ ent, const uint2 *__restrict__ tab,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N, int K,
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
             ell_stage<MT, WPG * 64, SB>(xs, X, M, K, m0, kc, C, tid, vec);
             __syncthreads();
         }
-        ell_walk<RPL, D>(y, q, e0, off, n8, n8pos, nmax, base);
+        ell_walk<RPL, D, LA>(y, q, e0, off, n8, n8pos, nmax, base);
     }
     if (slice >= nslices || n >= N) return;
     const float bn = b[n];
@@ -505,9 +505,9 @@ __global__ __launch_bounds__(64 * (MT + E / 8)) void tsg_tcsc_ell_pc_kernel(
 
 namespace {
 
-template <int LG, int RPL, int WPG>
-int launch_ell_t(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
-                 int M, int N, int K, int C, int nch, int prelu, hipStream_t s)
+template <int LG, int RPL, int WPG, int LA>
+int launch_ell_la(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
+                  int M, int N, int K, int C, int nch, int prelu, hipStream_t s)
 {
     constexpr int MT = LG * RPL, CPW = 64 / LG;
     const int nsg = (N + WPG * CPW - 1) / (WPG * CPW);
@@ -516,12 +516,31 @@ int launch_ell_t(const float *X, const uint4 *ent, const uint2 *tab, const float
     const size_t lds = (size_t)(C + 1) * MT * sizeof(float);
     const dim3 grid((unsigned)(nsg * mtiles)), block(WPG * 64);
     if (prelu)
-        hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, true>), grid, block, lds, s, X, ent, tab, b, alpha, Y,
-                           M, N, K, C, nch, steps, nsg);
+        hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, LA, true>), grid, block, lds, s, X, ent, tab, b, alpha,
+                           Y, M, N, K, C, nch, steps, nsg);
     else
-        hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, false>), grid, block, lds, s, X, ent, tab, b, alpha, Y,
-                           M, N, K, C, nch, steps, nsg);
+        hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, LA, false>), grid, block, lds, s, X, ent, tab, b, alpha,
+                           Y, M, N, K, C, nch, steps, nsg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// LDS lookahead of the walk (ell_walk): LA_DEFAULT, or TSG_ELL_LA=1/2 (A/B)
+int pick_la()
+{
+    static const int env = [] {
+        const char *v = getenv("TSG_ELL_LA");
+        const int x = v ? atoi(v) : 0;
+        return x == 1 || x == 2 ? x : 0;
+    }();
+    return env ? env : 1;
+}
+
+template <int LG, int RPL, int WPG>
+int launch_ell_t(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
+                 int M, int N, int K, int C, int nch, int prelu, hipStream_t s)
+{
+    if (pick_la() == 2) return launch_ell_la<LG, RPL, WPG, 2>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, prelu, s);
+    return launch_ell_la<LG, RPL, WPG, 1>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, prelu, s);
 }
 
 }  // namespace
