@@ -278,10 +278,13 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 //  * otherwise 2 x 16: the CU pairs that share an instruction cache on one
 //    code stream (configs[2] 1.212 ms vs 1.264 at 4 x 8; s = 2 2.554 vs 2.712).
 // TSG_JIT_GN / TSG_JIT_GM override (A/B).
-void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm)
+void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, int &tmask)
 {
     static const int env_gn = [] { const char *e = getenv("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
     static const int env_gm = [] { const char *e = getenv("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
+    // code touches: M tiles with (mt & tmask) == 0 spread them (tsg_jit_kernel.hip)
+    static const int env_tm = [] { const char *e = getenv("TSG_JIT_TMASK"); return e ? atoi(e) : -1; }();
+    tmask = env_tm >= 0 ? env_tm : 0;
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
     int n = 2, m = 16;
     if (ntiles <= 4 || mtiles <= 8 || density <= 0.1875) {
@@ -573,11 +576,12 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         slot = h->ring_head;
         HIP_TRY(hipEventRecord(h->ev0[slot], s));
     }
-    int gn = 2, gm = 16;
-    if (h->kind == tsg_tcsc::kJit) pick_jit_map(h, Mp / tsg::kJitTileM, jv->Npad / (jv->nw * jv->waves), gn, gm);
+    int gn = 2, gm = 16, tmask = 0;
+    if (h->kind == tsg_tcsc::kJit)
+        pick_jit_map(h, Mp / tsg::kJitTileM, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask);
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
-                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves, jv->waves, gn, gm, s)
+                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves, jv->waves, gn, gm, tmask, s)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)

@@ -126,7 +126,8 @@ struct JitModule {
 };
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
-                    int prelu, uint32_t *status, int tile_cols, int waves, int gn, int gm, void *stream);
+                    int prelu, uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask,
+                    void *stream);
 int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream);
 
 // ---------------------------------------------------------------------------

@@ -279,11 +279,12 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     }
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
-    // prefetch), nolgkm (no LDS waits), noreads (no X reads)
+    // prefetch), nolgkm (no LDS waits), noreads (no X reads), novm (the DMA
+    // pieces are never waited for: tells the DMA's latency from its issue cost)
     const std::string diag = std::getenv("TSG_JIT_DIAG") ? std::getenv("TSG_JIT_DIAG") : "";
     auto has = [&](const char *f) { return diag.find(f) != std::string::npos; };
     const bool d_nobar = has("nobar"), d_nodma = has("nodma"), d_notouch = has("notouch"),
-               d_nolgkm = has("nolgkm"), d_noreads = has("noreads");
+               d_nolgkm = has("nolgkm"), d_noreads = has("noreads"), d_novm = has("novm");
     // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,1)
     uint32_t touch_first = 1, touch_count = 1;
     if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
@@ -505,8 +506,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 if (dma && pieces_out < kPieces) pieces_upto(kPieces);
                 if (lag == 1) {
                     issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
-                    E.wait_vm(ntouch);  // this step's pieces (the touches may run on)
-                } else {
+                    if (!d_novm) E.wait_vm(ntouch);  // this step's pieces (the touches may run on)
+                } else if (!d_novm) {
                     // the previous step's pieces: only its touches and this
                     // step's operations may still be in flight
                     E.wait_vm(ntouch + (uint32_t)vm_step);
@@ -635,12 +636,12 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream)
 
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
-                    uint32_t *status, int tile_cols, int waves, int gn, int gm, void *stream)
+                    uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask, void *stream)
 {
     int mtiles = Mp / kJitTileM, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
-                      (void *)&status, (void *)&gn, (void *)&gm};
+                      (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask};
     hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.function, (unsigned)(mtiles * ntiles), 1, 1,
                                          (unsigned)waves * 64u, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;

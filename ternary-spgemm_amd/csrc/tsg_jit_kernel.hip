@@ -123,7 +123,8 @@ extern "C" __global__ __launch_bounds__(64) void tsg_jit_probe(uint32_t *__restr
 extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
-    int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm)
+    int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
+    int tmask)
 {
     __shared__ __attribute__((aligned(16))) char lds[kJRing * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -170,7 +171,11 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
         off[i] = (pr * ((uint32_t)Mp / 2u) + (uint32_t)m0 / 2u + (uint32_t)lane) * 16u - m0k * (uint32_t)(i & 3) * 1024u;
     }
     const uint32_t wb = (uint32_t)(wave * kJPieces) * 1024u;  // s83
-    const uint32_t l128 = (uint32_t)lane * 128u;
+    // code touch (one dword per 128-B line of the stream ahead, into L2): only
+    // workgroups with (mt & tmask) == 0 spread it over the lines; the others
+    // load one line 64 times (one request) -- the M tiles that run the same
+    // stream share what one of them touched (tsg_capi.cpp pick_jit_map)
+    const uint32_t l128 = (mt & tmask) == 0 ? (uint32_t)lane * 128u : 0u;
     const uint32_t stride = (uint32_t)kJChunk * (uint32_t)Mp * 4u;
 
 #define TSG_JIT_CALL(...)                                                                           \
