@@ -183,6 +183,19 @@ int tcsc_hip_jit_waves(const tsg_tcsc *h, int M);
 int tcsc_hip_set_small_m(tsg_tcsc *h, int mode);
 const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M);
 
+/* Far-X^T code image (no reference counterpart; DESIGN.md 4.1 "Long K"):
+ * calls that run the 64-wide weight-compiled kernel on its long-stream tile
+ * map (K >= 8192, density > 3/16) with an X^T far larger than the 256 MiB
+ * Infinity Cache (4 * M * K >= 768 MiB) and a code image that fits in it
+ * (8 * nnz <= 160 MiB) run a second image of the same code without
+ * code touches and with X^T staged by non-temporal loads, so the X^T stream
+ * does not evict the code the other column tiles re-read.  Same results bit
+ * for bit.  mode: 0 = automatic (default), 1 = never, 2 = every 64-wide call
+ * (tests).  Compiled on the first call that picks it (or tcsc_hip_reserve).
+ * tcsc_hip_call_far: 1 if a call with M rows runs it. */
+int tcsc_hip_set_far(tsg_tcsc *h, int mode);
+int tcsc_hip_call_far(const tsg_tcsc *h, int M);
+
 /* ---- introspection ------------------------------------------------------- */
 typedef struct tsg_info {
     int32_t K, N, device, abi_version;
@@ -277,6 +290,13 @@ int tsg_jit_codegen_wv(const int32_t *col_start_pos, const int32_t *col_start_ne
                        const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
                        int B, int width, int waves, uint32_t *code, int64_t code_cap, int64_t *code_len,
                        uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+
+/* The far-X^T image (tcsc_hip_set_far) of the 64-wide plain-TCSC code: no
+ * code touches, non-temporal LDS-DMA; region header word 7 bit 17 set. */
+int tsg_jit_codegen_far(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                        const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                        uint32_t *code, int64_t code_cap, int64_t *code_len,
+                        uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
 
 /* The weight-compiled kernel's tile map (tsg_jit_map.h): workgroup id L of a
  * grid of mtiles x ntiles -> (column tile *nt, M tile *mt) for groups of gn

@@ -50,7 +50,7 @@ struct tsg_tcsc {
         uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
         int64_t code_bytes = 0, wcode_words = 0;
     };
-    JitVariant jv[7];
+    JitVariant jv[8];                     // 7: the 64 x 8 "far X^T" image (pick_jit_shape)
     int jit_nch = 0;                      // X^T chunks (all widths)
     int jit_force = 0;                    // tcsc_hip_set_jit_width / TSG_JIT_NW: 0 = auto
     uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
@@ -63,6 +63,7 @@ struct tsg_tcsc {
         bool ready = false;
     };
     EllVariant ell[tsg::kEllVariants];
+    int far_mode = 0;                     // tcsc_hip_set_far: 0 auto, 1 never, 2 always (64 x 8 calls)
     int small_m = 0;                      // tcsc_hip_set_small_m: 0 auto, 1 never, 2 always, 3 always w/o pc (plain TCSC only)
     std::vector<int32_t> csp, csn, rip, rin;  // host TCSC (getVectorRepresentation)
     uint32_t *d_seg = nullptr, *d_ent = nullptr;
@@ -107,6 +108,9 @@ constexpr int kEllMidM = 32;
 constexpr int64_t kEllPcRowsMaxMN = 32768;
 constexpr int kEllStarvedMaxM = 1024;
 constexpr int64_t kJitFullWgs = 230;
+constexpr int64_t kJitOneRoundWgs = 256;  // one jit workgroup per CU (144 KiB of LDS)
+constexpr double kFarXtBytes = 768.0 * 1024 * 1024;  // X^T >= 3x the 256 MiB Infinity Cache
+constexpr double kFarCodeBytes = 160.0 * 1024 * 1024;  // code image well inside it
 constexpr int64_t kEllStarvedWgs = 64;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
 
@@ -202,17 +206,20 @@ int width_index(int nw)
     return -1;
 }
 
-// jv index of a (width, waves) shape: 8-wave widths 0..3, 4-wave widths 32/16/8 4..6
-int shape_index(int nw, int waves)
+// jv index of a (width, waves) shape: 8-wave widths 0..3, 4-wave widths
+// 32/16/8 4..6, the 64 x 8 far-X^T image 7
+int shape_index(int nw, int waves, bool far = false)
 {
     const int w = width_index(nw);
-    if (w < 0 || !tsg::jit_waves_ok(nw, waves)) return -1;
-    return waves == tsg::kJitWaves ? w : 3 + w;
+    if (w < 0 || !tsg::jit_waves_ok(nw, waves) || (far && (nw != tsg::kJitNW || waves != tsg::kJitWaves))) return -1;
+    return far ? 7 : waves == tsg::kJitWaves ? w : 3 + w;
 }
 
 struct JitShape {
     int nw, waves;
+    bool far = false;  // the far-X^T code image (tsg_jit.cpp build_jit_code)
 };
+int shape_index(const JitShape &sh) { return shape_index(sh.nw, sh.waves, sh.far); }
 
 // Shape (stream width x waves per workgroup) for a call with M rows.  Every
 // shape walks the same X^T chunks; a wider stream reads fewer LDS bytes per
@@ -226,6 +233,32 @@ struct JitShape {
 // M = 256, N = 16384: 32 x 4, 0.153 ms (16 x 8: 0.173); M >= 1024: 64 x 8.
 // A pinned width (tcsc_hip_set_jit_width) runs 8 waves; TSG_JIT_WAVES=4 forces
 // 4 waves for every narrow width (diagnostic).
+// The far-X^T image (no code touches, non-temporal X^T staging) for 64-wide
+// calls on the 1 x 32 tile map (long streams: K >= 8192, density > 3/16, more
+// than 4 column and 8 M tiles, pick_jit_map) whose X^T is far larger than the
+// 256 MiB Infinity Cache while the code fits in it: the X^T stream then no
+// longer evicts the code that every M tile of the XCD re-reads
+// (profiles/r03e_far_ab.txt, r03e_long_k_ab.txt, r03e_big_ab.txt, kernel ms):
+// (64000, 16384, 4096) s = 4 25.3-26.2 -> 21.6-22.2, (32000, 16384, 4096)
+// 12.3-12.4 -> 10.8-10.9, (16000, 16384, 4096) 5.9-6.1 -> 5.35-5.43,
+// (64000, 8192, 4096) 11.4-11.8 -> 10.8-10.9; it loses where X^T fits the
+// cache ((4096, 16384, 4096) 1.17 -> 1.50, (8192, ...) 2.63 -> 2.77), where
+// the code does not (s = 2: 38.9 -> 42.0) and on sparse W (s = 8 / 16: 4.9-9%
+// slower; those run the 4 x 8 map).  TSG_JIT_FAR=0/1 overrides.
+bool far_xt(const tsg_tcsc *h, int M)
+{
+    static const int env = [] { const char *e = getenv("TSG_JIT_FAR"); return e ? atoi(e) : -1; }();
+    if (h->B || h->far_mode == 1) return false;
+    if (h->far_mode == 2) return true;
+    if (h->jit_force) return false;
+    if (env >= 0) return env > 0;
+    const double nnz = (double)(h->nnz_pos + h->nnz_neg), density = nnz / std::max(1.0, (double)h->K * h->N);
+    const int64_t mtiles = ((int64_t)M + tsg::kJitTileM - 1) / tsg::kJitTileM,
+                  ntiles = ((int64_t)h->N + tsg::kJitTileCols - 1) / tsg::kJitTileCols;
+    const bool long_map = h->K >= 8192 && density > 0.1875 && ntiles > 4 && mtiles > 8;
+    return long_map && 4.0 * (double)M * (double)h->K >= kFarXtBytes && 8.0 * nnz <= kFarCodeBytes;
+}
+
 JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 {
     static const int env_waves = [] {
@@ -235,7 +268,7 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
     if (h->B) return {tsg::kJitNW, tsg::kJitWaves};
     if (h->jit_force) {
         const int w = env_waves == 4 && tsg::jit_waves_ok(h->jit_force, 4) ? 4 : tsg::kJitWaves;
-        return {h->jit_force, w};
+        return {h->jit_force, w, h->jit_force == tsg::kJitNW && w == tsg::kJitWaves && far_xt(h, M)};
     }
     const int64_t mt = (std::max(M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM;
     const double image8 = 8.0 * (double)(h->nnz_pos + h->nnz_neg);
@@ -261,7 +294,9 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
             }
         }
     }
-    return full ? best : most;
+    JitShape sh = full ? best : most;
+    sh.far = sh.nw == tsg::kJitNW && sh.waves == tsg::kJitWaves && far_xt(h, M);
+    return sh;
 }
 
 // Tile map groups (tsg_jit_map.h) per call: gn column tiles x gm M tiles per
@@ -277,14 +312,21 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 //    tile's code ((64000, 16384, 4096): 25.6 vs 26.8 ms);
 //  * otherwise 2 x 16: the CU pairs that share an instruction cache on one
 //    code stream (configs[2] 1.212 ms vs 1.264 at 4 x 8; s = 2 2.554 vs 2.712).
-// TSG_JIT_GN / TSG_JIT_GM override (A/B).
+// Code touches (tsg_jit_kernel.hip): only M tiles with (mt & tmask) == 0
+// spread theirs over the stream's lines.  When the whole grid is resident at
+// once (<= 256 workgroups: one per CU), the M tiles that run one column tile's
+// code run together, so one touch in four serves them (profiles/
+// r03e_touch_ab.txt, r03e_long_k_ab.txt: configs[1] 0.0989-0.1013 -> 0.0931-
+// 0.0938 ms, (1024, 4096, 1024) 0.0878 -> 0.0834, (1024, 16384, 1024) 0.317 ->
+// 0.303); with several rounds the touching tile may not run beside the others
+// (configs[2] +4%, s = 16 +15%, (256, 4096, 16384) +8%), so every tile touches.
+// TSG_JIT_GN / TSG_JIT_GM / TSG_JIT_TMASK override (A/B).
 void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, int &tmask)
 {
     static const int env_gn = [] { const char *e = getenv("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
     static const int env_gm = [] { const char *e = getenv("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
-    // code touches: M tiles with (mt & tmask) == 0 spread them (tsg_jit_kernel.hip)
     static const int env_tm = [] { const char *e = getenv("TSG_JIT_TMASK"); return e ? atoi(e) : -1; }();
-    tmask = env_tm >= 0 ? env_tm : 0;
+    tmask = env_tm >= 0 ? env_tm : ((int64_t)mtiles * ntiles <= kJitOneRoundWgs ? 3 : 0);
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
     int n = 2, m = 16;
     if (ntiles <= 4 || mtiles <= 8 || density <= 0.1875) {
@@ -309,9 +351,9 @@ int handle_stream(tsg_tcsc *h, hipStream_t &s)
 // or the first call that picks it) and runs its probe on `s` -- the call's
 // stream, or the handle's own non-blocking stream (nullptr) -- and
 // synchronises that stream only.  Caller holds h->mu (or owns h exclusively).
-int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStream_t s = nullptr)
+int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStream_t s = nullptr, bool far = false)
 {
-    const int i = shape_index(nw, waves);
+    const int i = shape_index(nw, waves, far);
     if (i < 0 || !tsg::jit_width_ok(nw))
         return fail(TSG_ERR_ARG, "unsupported jit stream width " + std::to_string(nw) + " x " + std::to_string(waves) +
                                  " waves");
@@ -319,7 +361,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
     if (v.mod.function) return TSG_OK;
     tsg::JitImage img;
     tsg::build_jit_code(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
-                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw, waves);
+                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw, waves, far);
     // stream offsets (wcode) and the dispatcher's region literal are 32-bit
     if ((uint64_t)img.code.size() * 4 >= (1ull << 32) - (1ull << 20))
         return fail(TSG_ERR_RANGE, "jit image of " + std::to_string((uint64_t)img.code.size() * 4) +
@@ -547,11 +589,11 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     tsg_tcsc::JitVariant *jv = nullptr;
     if (h->kind == tsg_tcsc::kJit) {
         const JitShape sh = pick_jit_shape(h, M);
-        jv = &h->jv[shape_index(sh.nw, sh.waves)];
+        jv = &h->jv[shape_index(sh)];
         if (!jv->mod.function && capturing)
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(sh.nw) +
                                          " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
-        rc = ensure_jit_variant(h, sh.nw, sh.waves, s);
+        rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far);
         if (rc) return rc;
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
@@ -1013,7 +1055,7 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
         if (pick_ell_variant(h, m) >= 0 && pick_ell_variant(h, std::min(m, (mt - 1) * tsg::kJitTileM + 1)) >= 0)
             continue;  // every M of this tile runs the small-M kernel
         const JitShape sh = pick_jit_shape(h, m);
-        rc = ensure_jit_variant(h, sh.nw, sh.waves);
+        rc = ensure_jit_variant(h, sh.nw, sh.waves, nullptr, sh.far);
         if (rc) return rc;
     }
     // the small-M images calls with M <= max_M run: the choice only changes
@@ -1089,6 +1131,21 @@ extern "C" int tcsc_hip_host_chunk_rows(tsg_tcsc *h, int M)
     return host_chunk_rows(h, M);
 }
 
+extern "C" int tcsc_hip_set_far(tsg_tcsc *h, int mode)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    if (mode < 0 || mode > 2) return fail(TSG_ERR_ARG, "tcsc_hip_set_far: expected 0 (auto), 1 (never) or 2 (always)");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->far_mode = mode;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_call_far(const tsg_tcsc *h, int M)
+{
+    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
+    return pick_jit_shape(h, M).far ? 1 : 0;
+}
+
 extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)
 {
     if (!h) return fail(TSG_ERR_ARG, "null handle");
@@ -1118,7 +1175,7 @@ extern "C" int64_t tcsc_hip_call_image_bytes(tsg_tcsc *h, int M)
     if (ev >= 0) return h->ell[ev].ready ? h->ell[ev].bytes : 0;
     if (h->kind != tsg_tcsc::kJit) return (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
     const JitShape sh = pick_jit_shape(h, M);
-    const tsg_tcsc::JitVariant &v = h->jv[shape_index(sh.nw, sh.waves)];
+    const tsg_tcsc::JitVariant &v = h->jv[shape_index(sh)];
     return v.mod.function ? v.code_bytes + v.wcode_words * 4 : 0;
 }
 

@@ -94,6 +94,9 @@ constexpr uint32_t kJitFormat = 2;                      // region header word 7 
 // the instruction offset field (one M0 per 4 pieces); the dispatcher then
 // subtracts (piece & 3) KiB from its per-piece global offsets
 constexpr uint32_t kJitM0kFlag = 1u << 16;
+// region header word 7 bit 17: the far-X^T image -- no code touches, X^T
+// staged with non-temporal loads (tsg_capi.cpp far_xt)
+constexpr uint32_t kJitFarFlag = 1u << 17;
 
 // Stream width: columns per generated stream.  kJitNW (64) is the default;
 // narrower streams (32, 16, 8: same register contract, fewer accumulators,
@@ -115,7 +118,7 @@ struct JitImage {
 // (comp.h:607-658) from BlockedTCSC<B> arrays
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                     const int32_t *rin, int K, int N, int B, JitImage &img, int nw = kJitNW,
-                    int waves = kJitWaves);
+                    int waves = kJitWaves, bool far = false);
 
 struct JitModule {
     void *module = nullptr;        // hipModule_t

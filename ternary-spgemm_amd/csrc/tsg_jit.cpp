@@ -203,7 +203,7 @@ std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw)
 }  // namespace
 
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
-                    int K, int N, int B, JitImage &img, int nw, int waves)
+                    int K, int N, int B, JitImage &img, int nw, int waves, bool far)
 {
     if (nw <= 0) nw = kJitNW;
     if (!jit_waves_ok(nw, waves)) waves = kJitWaves;
@@ -267,7 +267,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)waves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
                              (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
-                             (uint32_t)kJitRing | kJitFormat << 8 | (uint32_t)(m0k ? kJitM0kFlag : 0u)});
+                             (uint32_t)kJitRing | kJitFormat << 8 | (uint32_t)(m0k ? kJitM0kFlag : 0u) |
+                                 (far ? kJitFarFlag : 0u)});
     Emit E{code, std::getenv("TSG_JIT_NOALIGN") == nullptr};
     // TSG_JIT_CP="dma,touch": cache-policy bits of the LDS-DMA pieces and the
     // code touches (hex; 0x20000 = nt, 0x2000000 = sc1, 0x10000 = sc0; A/B)
@@ -277,6 +278,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         E.dma_cp = a & 0x2030000u;
         E.touch_cp = t & 0x2030000u;
     }
+    // far-X^T image (tsg_capi.cpp far_xt): X^T staged non-temporally so its
+    // stream does not evict the code from the Infinity Cache, and no code
+    // touches
+    if (far) E.dma_cp |= 0x20000u;
     // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
     // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
     // prefetch), nolgkm (no LDS waits), noreads (no X reads), novm (the DMA
@@ -291,7 +296,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     if (touch_count > 4) touch_count = 4;
     // the prefetch must stay inside the tail padding past the last stream
     if ((touch_first + touch_count) * 8192u > (uint32_t)kTailPad * 4u) touch_first = (uint32_t)kTailPad * 4u / 8192u - touch_count;
-    const uint32_t ntouch = d_notouch ? 0u : touch_count;
+    const uint32_t ntouch = d_notouch || far ? 0u : touch_count;
 
     int n0 = 0;  // first column of the current stream
     std::vector<int32_t> cur((size_t)nw * 2), end((size_t)nw * 2);
@@ -681,6 +686,28 @@ extern "C" int tsg_jit_codegen_wv(const int32_t *csp, const int32_t *csn, const 
     if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
     if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
         g_tsg_host_err = "tsg_jit_codegen: buffer too small";
+        return TSG_ERR_ARG;
+    }
+    if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);
+    if (wcode) std::memcpy(wcode, img.wcode.data(), img.wcode.size() * 4);
+    return TSG_OK;
+}
+
+extern "C" int tsg_jit_codegen_far(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                                   int K, int N, uint32_t *code, int64_t code_cap, int64_t *code_len, uint32_t *wcode,
+                                   int64_t wcode_cap, int64_t *wcode_len)
+{
+    const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, 0);
+    if (!e.empty()) {
+        g_tsg_host_err = "tsg_jit_codegen_far: malformed TCSC: " + e;
+        return TSG_ERR_ARG;
+    }
+    tsg::JitImage img;
+    tsg::build_jit_code(csp, csn, rip, rin, K, N, 0, img, tsg::kJitNW, tsg::kJitWaves, true);
+    if (code_len) *code_len = (int64_t)img.code.size();
+    if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
+    if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
+        g_tsg_host_err = "tsg_jit_codegen_far: buffer too small";
         return TSG_ERR_ARG;
     }
     if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);

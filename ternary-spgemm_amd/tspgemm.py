@@ -43,7 +43,8 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_jit_width", "tcsc_hip_set_jit_width", "tcsc_hip_jit_waves", "tsg_jit_codegen_w", "tsg_jit_codegen_wv",
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
-    "tcsc_hip_host_register", "tcsc_hip_host_unregister",
+    "tcsc_hip_host_register", "tcsc_hip_host_unregister", "tcsc_hip_set_far", "tcsc_hip_call_far",
+    "tsg_jit_codegen_far",
 )
 
 
@@ -126,6 +127,10 @@ def lib() -> C.CDLL:
     L.tsg_jit_codegen_wv.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                      C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tcsc_hip_set_small_m.argtypes = [H, C.c_int]
+    L.tcsc_hip_set_far.argtypes = [H, C.c_int]
+    L.tcsc_hip_call_far.argtypes = [H, C.c_int]
+    L.tsg_jit_codegen_far.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
+                                      C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tcsc_hip_set_host_chunks.argtypes = [H, C.c_int]
     L.tcsc_hip_host_chunk_rows.argtypes = [H, C.c_int]
     L.tcsc_hip_call_image_bytes.argtypes = [H, C.c_int]
@@ -252,6 +257,21 @@ def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0, width: int = 64,
     _check(L.tsg_jit_codegen_wv(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, B, width, waves, _ptr(code),
                                 nc.value, C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)),
            "tsg_jit_codegen")
+    return code, wcode
+
+
+def jit_codegen_far(csp, csn, rip, rin, K: int, N: int):
+    """The far-X^T image of the 64-wide plain-TCSC code (no code touches,
+    non-temporal X^T staging; include/ternary_spgemm.h tcsc_hip_set_far)."""
+    csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
+    nc, nw = C.c_int64(), C.c_int64()
+    L = lib()
+    _check(L.tsg_jit_codegen_far(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, None, 0, C.byref(nc), None, 0,
+                                 C.byref(nw)), "tsg_jit_codegen_far")
+    code = np.empty(nc.value, np.uint32)
+    wcode = np.empty(nw.value, np.uint32)
+    _check(L.tsg_jit_codegen_far(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, _ptr(code), nc.value,
+                                 C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)), "tsg_jit_codegen_far")
     return code, wcode
 
 
@@ -569,6 +589,15 @@ class TCSCDevice:
     def call_kernel(self, M: int) -> str:
         """Device kernel a call with M rows launches."""
         return lib().tcsc_hip_call_kernel(self._h, M).decode()
+
+    def set_far(self, mode: int) -> None:
+        """Far-X^T code image: 0 = automatic (default), 1 = never, 2 = every
+        64-wide call."""
+        _check(lib().tcsc_hip_set_far(self._h, mode), "tcsc_hip_set_far")
+
+    def call_far(self, M: int) -> bool:
+        """True if a call with M rows runs the far-X^T image."""
+        return bool(lib().tcsc_hip_call_far(self._h, M))
 
     def info(self) -> dict:
         o = tsg_info()

@@ -108,6 +108,35 @@ def test_every_stream_width_vs_oracle(tsg, oracle_mod, width):
         h.close()
 
 
+def test_far_image_vs_oracle(tsg, oracle_mod):
+    """The far-X^T image (tcsc_hip_set_far: no code touches, non-temporal X^T
+    staging) on ragged shapes, bit for bit against the oracle and the default
+    image; the automatic rule keeps small calls on the default image."""
+    O = oracle_mod
+    for M, K, N, s in ((129, 257, 600, 4), (300, 1000, 1100, 16), (5, 96, 520, 2)):
+        W = O.gen_ternary(K, N, s, 3 * M + K)
+        t = O.tcsc_encode(W)
+        h = tsg.TCSCDevice(*t.arrays, K, N)
+        h.set_small_m(1)
+        h.set_jit_width(64)
+        assert not h.call_far(M)  # X^T far below the Infinity Cache: the default image
+        b = (np.arange(N, dtype=np.float32) - N / 3) * 0.21
+        alpha = np.linspace(-0.5, 0.5, N).astype(np.float32)
+        Xs = (O.init_x_int(M, K, 15), O.init_x_frac(M, K, 16))
+        base = [h.gemm(X, b) for X in Xs]
+        h.set_far(2)
+        assert h.call_far(M) and h.call_kernel(M) == "tsg_jit_kernel"
+        for X, Yb in zip(Xs, base):
+            Y = h.gemm(X, b)
+            assert _bits_eq(Y, Yb) and _bits_eq(Y, O.base_tcsc(X, t, b)), (M, K, N, s)
+            assert _bits_eq(h.gemm_prelu(X, b, alpha), O.base_tcsc_prelu(X, t, b, alpha))
+        h.set_far(1)
+        assert not h.call_far(M)
+        with pytest.raises(tsg.TSGError):
+            h.set_far(3)
+        h.close()
+
+
 def test_auto_width_small_m(tsg, oracle_mod):
     """Automatic width: narrow streams for small M, the default 64 at config
     3's M; one handle switching widths call by call stays bit-exact."""

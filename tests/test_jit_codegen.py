@@ -38,7 +38,7 @@ class Geom:
         # DMA pieces take their in-group offset from the instruction offset (one
         # M0 per 4 pieces; the dispatcher subtracts it from the global offsets)
         self.m0k = (int(code[7]) >> 16) & 1
-        assert int(code[7]) >> 17 == 0
+        assert int(code[7]) >> 18 == 0  # bit 16: m0k, bit 17: far-X^T image
         self.pairs = self.chunk // 2                  # k-row pairs per chunk
         self.pair_bytes = self.tile_m * 8             # one pair row of the tile in LDS: 1 KiB
         self.buf_bytes = self.pairs * self.pair_bytes
@@ -314,6 +314,29 @@ def test_jit_code_four_wave_workgroups(tsg, oracle_mod, M, K, N, s, width):
     (lane*128 v120, accumulators from v122), twice the column tiles; same order."""
     for frac in (False, True):
         _check(tsg, oracle_mod, M, K, N, s, 7 + K + N + width, frac, width=width, waves=4)
+
+
+@pytest.mark.parametrize("M,K,N,s", [(5, 70, 33, 2), (130, 300, 520, 4), (3, 97, 9, 16)])
+def test_jit_code_far_image(tsg, oracle_mod, M, K, N, s):
+    """The far-X^T image (tcsc_hip_set_far): the default 64-wide code with the
+    code touches removed and every X^T DMA piece non-temporal (nt bit), header
+    word 7 bit 17 -- nothing else differs, so the same order."""
+    O = oracle_mod
+    W = O.gen_ternary(K, N, s, 3 + K)
+    t = O.tcsc_encode(W)
+    code, wcode = tsg.jit_codegen_far(*t.arrays, K, N)
+    base, _ = tsg.jit_codegen(*t.arrays, K, N)
+    assert int(code[7]) & (1 << 17) and not int(base[7]) & (1 << 17)
+    words = [int(w) for w in code]
+    n_dma = sum(1 for w in words if (w & ~0x2030000 & 0xFFFFF000) == 0xDDF48000)
+    assert n_dma > 0 and n_dma == sum(1 for w in words if (w & 0xFFFFF000) == 0xDDF48000 | 0x20000)
+    assert not any((w & ~0x2030000) == 0xDC508000 for w in words)  # no code touch
+    for frac in (False, True):
+        X = O.init_x_frac(M, K, 9) if frac else O.init_x_int(M, K, 9)
+        b = np.linspace(-2, 3, N).astype(np.float32)
+        Y = emulate(code, wcode, X, K, N) + b
+        ref = O.base_tcsc(X, t, b)
+        assert np.array_equal(Y.view(np.uint32), ref.view(np.uint32)), (M, K, N, s, frac)
 
 
 def test_jit_width_rejected(tsg, oracle_mod):
