@@ -308,8 +308,9 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 //  * sparse W (density <= 3/16, s >= 8): 4 x 8 -- a column tile's code is
 //    short, so sharing each X^T slab between more column tiles wins (s = 16:
 //    0.565 vs 0.604 ms at 2 x 16; s = 8: 0.769 vs 0.792);
-//  * long streams (K >= 8192): 1 x 32, every CU of the XCD on one column
-//    tile's code ((64000, 16384, 4096): 25.6 vs 26.8 ms);
+//  * long streams (K >= 8192, density > 3/32): 1 x 32, every CU of the XCD on
+//    one column tile's code ((64000, 16384, 4096): 25.6 vs 26.8 ms; s = 8
+//    13.7 vs 15.3-15.8 ms);
 //  * otherwise 2 x 16: the CU pairs that share an instruction cache on one
 //    code stream (configs[2] 1.212 ms vs 1.264 at 4 x 8; s = 2 2.554 vs 2.712).
 // Code touches (tsg_jit_kernel.hip): only M tiles with (mt & tmask) == 0
@@ -329,7 +330,11 @@ void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, i
     tmask = env_tm >= 0 ? env_tm : ((int64_t)mtiles * ntiles <= kJitOneRoundWgs ? 3 : 0);
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
     int n = 2, m = 16;
-    if (ntiles <= 4 || mtiles <= 8 || density <= 0.1875) {
+    // s = 8 over long K takes the long-stream map ((64000, 16384, 4096) s = 8:
+    // 13.72-13.73 ms vs 15.3-15.8 at 4 x 8, profiles/r03f_sparse_big_ab.txt);
+    // s = 16 stays on 4 x 8 (8.38-8.45 vs 11.66 at 1 x 32)
+    const bool long_sparse = h->K >= 8192 && density > 0.09375;
+    if (ntiles <= 4 || mtiles <= 8 || (density <= 0.1875 && !long_sparse)) {
         n = 4;
         m = 8;
     } else if (h->K >= 8192) {
