@@ -315,19 +315,20 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 //    code stream (configs[2] 1.212 ms vs 1.264 at 4 x 8; s = 2 2.554 vs 2.712).
 // Code touches (tsg_jit_kernel.hip): only M tiles with (mt & tmask) == 0
 // spread theirs over the stream's lines.  When the whole grid is resident at
-// once (<= 256 workgroups: one per CU), the M tiles that run one column tile's
-// code run together, so one touch in four serves them (profiles/
+// once (<= 256 workgroups: one per CU) and >= 4 M tiles share each stream,
+// those M tiles run together, so one touch in four serves them (profiles/
 // r03e_touch_ab.txt, r03e_long_k_ab.txt: configs[1] 0.0989-0.1013 -> 0.0931-
 // 0.0938 ms, (1024, 4096, 1024) 0.0878 -> 0.0834, (1024, 16384, 1024) 0.317 ->
 // 0.303); with several rounds the touching tile may not run beside the others
-// (configs[2] +4%, s = 16 +15%, (256, 4096, 16384) +8%), so every tile touches.
+// (configs[2] +4%, s = 16 +15%), and with 2 M tiles per stream it loses too
+// ((256, 4096, 16384) +7-17%, r03g_ref_cases.jsonl), so every tile touches.
 // TSG_JIT_GN / TSG_JIT_GM / TSG_JIT_TMASK override (A/B).
 void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, int &tmask)
 {
     static const int env_gn = [] { const char *e = getenv("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
     static const int env_gm = [] { const char *e = getenv("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
     static const int env_tm = [] { const char *e = getenv("TSG_JIT_TMASK"); return e ? atoi(e) : -1; }();
-    tmask = env_tm >= 0 ? env_tm : ((int64_t)mtiles * ntiles <= kJitOneRoundWgs ? 3 : 0);
+    tmask = env_tm >= 0 ? env_tm : ((int64_t)mtiles * ntiles <= kJitOneRoundWgs && mtiles >= 4 ? 3 : 0);
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
     int n = 2, m = 16;
     // s = 8 over long K takes the long-stream map ((64000, 16384, 4096) s = 8:
