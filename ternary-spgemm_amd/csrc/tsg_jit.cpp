@@ -246,7 +246,11 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     const int64_t nnz_all = B ? (int64_t)csp[(int64_t)(K / B) * N] + csn[(int64_t)(K / B) * N]
                               : (int64_t)csp[N] + csn[N];
     const double density = (double)nnz_all / std::max(1.0, (double)K * (double)N);
-    double dma_spread = K >= 8192 && density <= 0.1875 ? 0.0 : 0.5;
+    // dense W (density > 3/8, s = 2) on the 64-wide image: also 0 -- its long
+    // steps leave the late pieces too little time (configs[3] s = 2 2.535 ->
+    // 2.452 ms; the 32-wide image of (256, 4096, 16384) s = 2 loses 4% with
+    // it, profiles/r03g_s2_ab.txt)
+    double dma_spread = (K >= 8192 && density <= 0.1875) || (density > 0.375 && nw == kJitNW) ? 0.0 : 0.5;
     int m0k = 1, lag = 1;
     if (const char *dv = std::getenv("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d,%d", &dma_spread, &m0k, &lag);
     if (lag != 2) lag = 1;
