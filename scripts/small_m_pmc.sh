@@ -9,7 +9,7 @@ for CTR in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU S
            "FETCH_SIZE"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $CTR --output-format csv -d $OUT/p$i -o run -- \
-      python3 scripts/small_m_sweep.py --M 1,16 --reps 3 > $OUT/p$i.log 2>&1
+      python3 scripts/small_m_sweep.py --M ${SMALL_M_LIST:-16,64} --reps 3 > $OUT/p$i.log 2>&1
   echo "pass $i rc=$?"
 done
 python3 - $OUT <<'P'
