@@ -34,7 +34,8 @@ def _dense_w(csp, csn, rip, rin, K, N, dev):
     (4096, 4096, 16384, 16),
     (1000, 2048, 512, 4),        # reference cases (plots/run_benchmark.py:8-33)
     (16000, 8192, 2048, 8),
-    (64000, 16384, 4096, 4),     # the reference's largest case
+    (64000, 16384, 4096, 4),     # the reference's largest case (the far-X^T image)
+    (64000, 16384, 4096, 8),     # ... sparse, on the 1 x 32 map
     (37, 16384, 16384, 4),       # small M, K in several chunks
 ])
 def test_full_y_integer_x(tsg, M, K, N, s):
@@ -48,7 +49,9 @@ def test_full_y_integer_x(tsg, M, K, N, s):
     X = torch.randint(-512, 513, (M, K), generator=g, device=dev, dtype=torch.int32).to(torch.float32)
     b = torch.full((N,), 2.0, device=dev)  # main.cpp:194
     Y = h.gemm_torch(X, b)
-    kernel = h.call_kernel(M)
+    kernel = h.call_kernel(M) + (" (far-X^T image)" if h.call_far(M) else "")
+    # the automatic far-X^T rule (tsg_capi.cpp far_xt) picks the largest case at s = 4 only
+    assert h.call_far(M) == ((M, K, N, s) == (64000, 16384, 4096, 4))
     W = _dense_w(csp, csn, rip, rin, K, N, dev)
     ref = torch.matmul(X, W) + b
     del W
