@@ -445,8 +445,9 @@ def main():
             with_gather = {"ms_per_step": round(gather["pipeline_ms"], 4),
                            "value": round(flops_all / (gather["pipeline_ms"] * 1e-3) / 1e9, 3),
                            "unit": "GFLOP/s",
-                           "note": "compute + RCCL all-gather of Y into row-major [M, N_total], pipelined by "
-                                   f"{gather['chunks']} M chunks (tsg_dist.GatherPipeline)",
+                           "note": f"compute + {'RCCL' if backend == 'nccl' else backend} all-gather of Y into "
+                                   f"row-major [M, N_total], pipelined by {gather['chunks']} M chunks "
+                                   "(tsg_dist.GatherPipeline)",
                            "columns_match_compute_only": gather["columns_match"],
                            "bytes_received_per_gpu": gather["bytes_received_per_gpu"]}
         out = {
