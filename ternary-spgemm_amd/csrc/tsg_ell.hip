@@ -260,6 +260,14 @@ __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
             n8 = t.y & 0xffffu;
             n8pos = t.y >> 16;
         }
+        if constexpr (CPW == 16) {
+            // the wave is one slice: its stream offset, list length and sign
+            // split are uniform -- in SGPRs the refill addresses and the
+            // block signs need no per-lane compare / select
+            off = __builtin_amdgcn_readfirstlane(off);
+            n8 = __builtin_amdgcn_readfirstlane(n8);
+            n8pos = __builtin_amdgcn_readfirstlane(n8pos);
+        }
         uint4 q[D];
 #pragma unroll
         for (int d = 0; d < D; d++) q[d] = e0[(uint32_t)d < n8 ? (off + d) * 16 : 0];
