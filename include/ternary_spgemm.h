@@ -196,6 +196,15 @@ const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M);
 int tcsc_hip_set_far(tsg_tcsc *h, int mode);
 int tcsc_hip_call_far(const tsg_tcsc *h, int M);
 
+/* The automatic per-call plan (host only, no GPU) of a plain-TCSC handle with
+ * K, N and nnz nonzeros for a call with M rows -- the rules calls follow
+ * (DESIGN.md 4): *kernel 0 = weight-compiled, 1 = small-M walk, 2 = its
+ * producer/consumer form; for the weight-compiled kernel the stream width and
+ * waves per workgroup, the far-X^T image (0/1), the tile-map groups
+ * (gn column tiles x gm M tiles) and the code-touch mask. */
+int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int *width, int *waves, int *far,
+                  int *gn, int *gm, int *tmask);
+
 /* ---- introspection ------------------------------------------------------- */
 typedef struct tsg_info {
     int32_t K, N, device, abi_version;

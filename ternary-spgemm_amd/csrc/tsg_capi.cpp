@@ -1165,6 +1165,39 @@ extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)
     return TSG_OK;
 }
 
+// The automatic per-call plan of a plain-TCSC handle with K, N and nnz
+// nonzeros at density split evenly (host only, no GPU: the same functions
+// run_dev uses on a handle).  kernel: 0 weight-compiled, 1 ELL walk, 2 ELL
+// producer/consumer walk.
+extern "C" int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int *width, int *waves, int *far,
+                             int *gn, int *gm, int *tmask)
+{
+    if (K < 0 || N <= 0 || nnz < 0 || nnz > (int64_t)K * N || M <= 0 || !kernel || !width || !waves || !far ||
+        !gn || !gm || !tmask) {
+        g_tsg_host_err = "tsg_call_plan: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    tsg_tcsc h;  // plain struct: nothing allocated, nothing on the device
+    h.K = K;
+    h.N = N;
+    h.nnz_pos = nnz - nnz / 2;
+    h.nnz_neg = nnz / 2;
+    h.jit_nch = std::max(1, (K + tsg::kJitChunk - 1) / tsg::kJitChunk);
+    const int ev = pick_ell_variant(&h, M);
+    *kernel = ev < 0 ? 0 : use_ell_pc(&h, ev) ? 2 : 1;
+    *width = *waves = *far = *gn = *gm = *tmask = 0;
+    if (ev < 0) {
+        const JitShape sh = pick_jit_shape(&h, M);
+        const int Mp = (M + tsg::kJitTileM - 1) / tsg::kJitTileM * tsg::kJitTileM;
+        const int ntiles = (N + sh.nw * sh.waves - 1) / (sh.nw * sh.waves);
+        *width = sh.nw;
+        *waves = sh.waves;
+        *far = sh.far ? 1 : 0;
+        pick_jit_map(&h, Mp / tsg::kJitTileM, ntiles, *gn, *gm, *tmask);
+    }
+    return TSG_OK;
+}
+
 extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)
 {
     if (!h) return "";

@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
     "tcsc_hip_host_register", "tcsc_hip_host_unregister", "tcsc_hip_set_far", "tcsc_hip_call_far",
-    "tsg_jit_codegen_far",
+    "tsg_jit_codegen_far", "tsg_call_plan",
 )
 
 
@@ -128,6 +128,7 @@ def lib() -> C.CDLL:
                                      C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tcsc_hip_set_small_m.argtypes = [H, C.c_int]
     L.tcsc_hip_set_far.argtypes = [H, C.c_int]
+    L.tsg_call_plan.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int] + [C.POINTER(C.c_int)] * 7
     L.tcsc_hip_call_far.argtypes = [H, C.c_int]
     L.tsg_jit_codegen_far.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
                                       C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
@@ -273,6 +274,17 @@ def jit_codegen_far(csp, csn, rip, rin, K: int, N: int):
     _check(L.tsg_jit_codegen_far(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, _ptr(code), nc.value,
                                  C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)), "tsg_jit_codegen_far")
     return code, wcode
+
+
+def call_plan(K: int, N: int, nnz: int, M: int) -> dict:
+    """The automatic per-call plan of a plain-TCSC handle (host only):
+    kernel, jit stream width x waves, far-X^T image, tile-map groups and
+    code-touch mask (include/ternary_spgemm.h tsg_call_plan)."""
+    v = [C.c_int() for _ in range(7)]
+    _check(lib().tsg_call_plan(K, N, nnz, M, *[C.byref(x) for x in v]), "tsg_call_plan")
+    kernel, width, waves, far, gn, gm, tmask = (x.value for x in v)
+    return {"kernel": ("tsg_jit_kernel", "tsg_tcsc_ell_kernel", "tsg_tcsc_ell_pc_kernel")[kernel],
+            "width": width, "waves": waves, "far": bool(far), "map": (gn, gm), "tmask": tmask}
 
 
 def jit_tile_map(L: int, mtiles: int, ntiles: int, gn: int, gm: int):

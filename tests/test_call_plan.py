@@ -1,0 +1,54 @@
+"""The automatic per-call plan (tsg_call_plan, host only): which kernel, stream
+shape, code image, tile map and code-touch mask a call takes.  Each expected
+plan is the measured winner recorded in DESIGN.md section 4 (profiles/ named
+per case), so a change of the rules that moves a BASELINE config or a
+reference case off its measured best shows up here, before any GPU runs."""
+import pytest
+
+
+@pytest.mark.parametrize("shape,plan", [
+    # configs[2] (the bench): 64 x 8, CU pairs on one code stream (2 x 16)
+    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(2, 16), tmask=0)),
+    # configs[1]: 16 x 4 one-round grid, code touches thinned (r03e_touch_ab.txt, r03q_mid_shape_ab.txt)
+    ((512, 4096, 4096, 4), dict(kernel="tsg_jit_kernel", width=16, waves=4, far=False, map=(4, 4), tmask=3)),
+    # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt)
+    ((4096, 4096, 16384, 16), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=0)),
+    # the reference's largest case: s = 4 far-X^T image on 1 x 32 (r03e_far_ab.txt) ...
+    ((64000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
+    # ... s = 2 (code past the Infinity Cache) and s = 8 default image on 1 x 32 (r03f_sparse_big_ab.txt) ...
+    ((64000, 16384, 4096, 2), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
+    ((64000, 16384, 4096, 8), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
+    # ... s = 16 on 4 x 8
+    ((64000, 16384, 4096, 16), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=0)),
+    # X^T too small for the far image (r03e_long_k_ab.txt) / large enough
+    ((8192, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
+    ((16000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
+    # 2 M tiles per stream: every tile touches (r03g_ref_cases.jsonl)
+    ((256, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=32, waves=4, far=False, map=(4, 2), tmask=0)),
+    ((1024, 4096, 1024, 4), dict(kernel="tsg_jit_kernel", width=8, waves=4, far=False, map=(4, 8), tmask=3)),
+])
+def test_plan_matches_measured_winners(tsg, shape, plan):
+    M, K, N, s = shape
+    got = tsg.call_plan(K, N, K * N // s, M)
+    assert got == plan, (shape, got)
+
+
+@pytest.mark.parametrize("M,K,N,kernel", [
+    (1, 4096, 16384, "tsg_tcsc_ell_pc_kernel"),   # M = 1: producer/consumer walk
+    (16, 4096, 16384, "tsg_tcsc_ell_kernel"),     # small M: the sliced-ELL walk
+    (64, 4096, 16384, "tsg_tcsc_ell_kernel"),     # up to 64 while an 8-row tile holds K
+    (96, 4096, 16384, "tsg_jit_kernel"),
+    (32, 1024, 4096, "tsg_tcsc_ell_kernel"),      # configs[0]
+    (32, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 32
+    (40, 16384, 16384, "tsg_jit_kernel"),
+    (1000, 2048, 512, "tsg_tcsc_ell_kernel"),     # starved jit grid (<= 64 workgroups)
+])
+def test_plan_small_m_kernel(tsg, M, K, N, kernel):
+    assert tsg.call_plan(K, N, K * N // 4, M)["kernel"] == kernel
+
+
+def test_plan_rejects_bad_arguments(tsg):
+    with pytest.raises(tsg.TSGError):
+        tsg.call_plan(64, 0, 0, 1)
+    with pytest.raises(tsg.TSGError):
+        tsg.call_plan(64, 64, 64 * 64 + 1, 1)
