@@ -82,6 +82,7 @@ def main():
                           "gflops_kernel": round(adds / (ms * 1e-3) / 1e9, 1),
                           "valu_frac": round(adds / (ms * 1e-3) / 78.64e12, 4),
                           "jit_width": jw, "jit_waves": h.jit_waves(M), "width_pinned": bool(width),
+                          "far_image": h.call_far(M),
                           "workgroups": -(-M // 128) * -(-N // (h.jit_waves(M) * max(jw, 1))),
                           "register_s": round(reg_s, 2),
                           "bit_identical_rows": ok}), flush=True)
