@@ -17,11 +17,14 @@
 // libref.so).  tests/test_integration_ref.py builds it on the CPU (compile +
 // link = the ABI and the interface match); tests/test_gpu_parity.py runs it
 // on the GPU when present.  Without a device it only reports that it linked.
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -47,6 +50,15 @@ void add_prelu_function(comp_func_prelu f, std::string name)
 {
     userFuncs_prelu.push_back(f);
     funcNames_prelu.push_back(name);
+}
+
+// threads for the reference GEMMs: OMP_NUM_THREADS (the GPU box's CPU share,
+// 16) or the host's cores, at most 16 and one row block per thread at least
+static unsigned ref_threads(int M)
+{
+    unsigned n = std::thread::hardware_concurrency();
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) n = (unsigned)std::max(1, std::atoi(e));
+    return std::max(1u, std::min({n, 16u, (unsigned)std::max(M, 1)}));
 }
 
 int main(int argc, char **argv)
@@ -92,14 +104,30 @@ int main(int argc, char **argv)
     std::vector<float> Y_main(M * N, 0);
     std::vector<float> refY_main(M * N, 0);
     std::vector<float> refY_prelu_main(M * N, 0);
-    GEMM(X_main.data(), W_FP32_main.data(), B_main.data(), refY_main.data(), M, N, K);
-    GEMM_PreLU(X_main.data(), W_FP32_main.data(), B_main.data(), alpha_main.data(), refY_prelu_main.data(), M, N, K);
     // BlockedTCSC<512> drops rows past (K/512)*512 (BlockedTCSC.h:17): its reference is
     // the GEMM of that truncated W
     std::vector<float> W_blk(W_FP32_main);
     for (size_t i = (size_t)(K / 512) * 512 * N; i < W_blk.size(); i++) W_blk[i] = 0;
     std::vector<float> refY_blk(M * N, 0);
-    GEMM(X_main.data(), W_blk.data(), B_main.data(), refY_blk.data(), M, N, K);
+    // The reference's serial GEMM / GEMM_PreLU (sparseUtils.h:92-129), unchanged,
+    // called on row blocks from several threads: every row of Y depends only on
+    // its row of X, so the result is the one serial call's, bit for bit (at
+    // configs[1] the three serial GEMMs take minutes on one core)
+    const unsigned nt = ref_threads(M);
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nt; t++) {
+        const int r0 = (int)((int64_t)M * t / nt), r1 = (int)((int64_t)M * (t + 1) / nt);
+        if (r1 <= r0) continue;
+        pool.emplace_back([&, r0, r1] {
+            float *x = X_main.data() + (size_t)r0 * K;
+            GEMM(x, W_FP32_main.data(), B_main.data(), refY_main.data() + (size_t)r0 * N, r1 - r0, N, K);
+            GEMM_PreLU(x, W_FP32_main.data(), B_main.data(), alpha_main.data(), refY_prelu_main.data() + (size_t)r0 * N,
+                       r1 - r0, N, K);
+            GEMM(x, W_blk.data(), B_main.data(), refY_blk.data() + (size_t)r0 * N, r1 - r0, N, K);
+        });
+    }
+    for (auto &th : pool) th.join();
+    std::printf("reference GEMM / GEMM_PreLU done on %u thread(s) (M=%d K=%d N=%d s=%d)\n", nt, M, K, N, s);
 
     for (size_t i = 0; i < userFuncs.size(); i++) {
         std::fill(Y_main.begin(), Y_main.end(), 0);

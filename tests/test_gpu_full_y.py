@@ -8,7 +8,9 @@ That makes a dense fp32 GEMM on the GPU (torch.matmul of X and the dense
 +-1 W) an exact reference for the whole [M, N] result at full size -- the
 same argument the reference's own correctness check rests on (main.cpp:206-227
 compares BaseTCSC against its dense GEMM).  Order for non-integer X is pinned
-by the sampled-row oracle tests (test_gpu_parity.py, test_gpu_sweep.py).
+on every element too (test_full_y_fractional_x): the oracle's BaseTCSC
+restatement, OpenMP over rows, at configs[1], configs[2] and configs[3]
+s = 2/8/16.
 """
 import numpy as np
 import pytest
@@ -60,3 +62,43 @@ def test_full_y_integer_x(tsg, M, K, N, s):
     bad = int((Y.view(torch.int32) != ref.view(torch.int32)).sum()) if not same else 0
     h.close()
     assert same, f"{bad} of {M * N} elements differ ({kernel})"
+
+
+def _oracle_threads() -> int:
+    """The GPU box's CPU share (OMP_NUM_THREADS = 16 there), at most 16."""
+    import os
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(16, n or len(os.sched_getaffinity(0))))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("M,K,N,s", [
+    (512, 4096, 4096, 4),        # configs[1]
+    (4096, 4096, 16384, 4),      # configs[2] (the bench workload)
+    (4096, 4096, 16384, 2),      # configs[3]
+    (4096, 4096, 16384, 8),
+    (4096, 4096, 16384, 16),
+    (64, 4096, 16384, 4),        # small M at configs[2]'s K, N
+])
+def test_full_y_fractional_x(tsg, oracle_mod, M, K, N, s):
+    """Order-sensitive X (mantissas of 24 bits over a 2^-23..2^0 exponent
+    spread: every partial sum rounds) at full BASELINE sizes, EVERY element
+    compared bitwise with the BaseTCSC restatement (oracle/tcsc_oracle.c,
+    comp.h:37-63) run over all M rows with OpenMP -- the accumulation order
+    pinned on the whole result, not on sampled rows."""
+    import torch
+    O = oracle_mod
+    csp, csn, rip, rin = tsg.gen_tcsc(K, N, s, 42)
+    t = O.TCSC(csp, csn, rip, rin, K, N)
+    X = O.init_x_frac(M, K, 7 + s)
+    b = (np.arange(N, dtype=np.float32) % 13 - 6) * np.float32(0.37)
+    h = tsg.TCSCDevice(csp, csn, rip, rin, K, N, device=0)
+    kernel = h.call_kernel(M)
+    Y = h.gemm_torch(torch.from_numpy(X).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+    h.close()
+    ref = O.base_tcsc(X, t, b, threads=_oracle_threads())
+    diff = Y.view(np.uint32) != ref.view(np.uint32)
+    assert not diff.any(), f"{int(diff.sum())} of {M * N} elements differ ({kernel}); first at {np.argwhere(diff)[0]}"

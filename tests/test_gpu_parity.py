@@ -432,8 +432,14 @@ def test_plugin_against_reference_headers():
     exe = os.path.join(REPO, "oracle", "_ref", "plugin_ref_check")
     if not os.path.exists(exe):
         pytest.skip("plugin_ref_check not built (needs the reference headers in the build container)")
-    for argv in ([], ["-M", "130", "-K", "1100", "-N", "300", "-s", "2"]):
-        r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=120)
+    # main.cpp:49-52 argv; the last two are BASELINE configs[0] (M=32 K=1024
+    # N=4096 s=4, "./sparseGEMM.out -correctness") and configs[1] (M=512
+    # K=4096 N=4096 s=4): the reference's own generator, ctors, serial dense
+    # GEMM and compare_results (main.cpp:192-247) around the HIP comp_funcs
+    for argv in ([], ["-M", "130", "-K", "1100", "-N", "300", "-s", "2"],
+                 ["-M", "32", "-K", "1024", "-N", "4096", "-s", "4"],
+                 ["-M", "512", "-K", "4096", "-N", "4096", "-s", "4"]):
+        r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=400)
         assert r.returncode == 0, r.stdout + r.stderr
         for name in ("HipBaseTCSC", "HipBaseBlockedTCSC", "HipBaseTCSC_PreLU"):
             assert f"Test case {name} passed!" in r.stdout, r.stdout
