@@ -1,4 +1,6 @@
 #!/bin/bash
+# TSG_JIT_DIAG code variants exist only in the diagnostic build (make -C ternary-spgemm_amd diag)
+export TSG_LIB=${TSG_LIB:-ternary-spgemm_amd/lib/libternary_spgemm_diag.so}
 # GPU box: where (64000, 16384, 4096) s=4 waits -- kernel time of the
 # TSG_JIT_DIAG code variants (tsg_jit.cpp; results WRONG, timing only).
 # Usage: scripts/big_diag.sh <out>

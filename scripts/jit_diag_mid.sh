@@ -1,4 +1,6 @@
 #!/bin/bash
+# TSG_JIT_DIAG code variants exist only in the diagnostic build (make -C ternary-spgemm_amd diag)
+export TSG_LIB=${TSG_LIB:-ternary-spgemm_amd/lib/libternary_spgemm_diag.so}
 # GPU box: where the per-step time of the weight-compiled kernel goes at mid M
 # (configs[1], M = 256, M = 64 forced to jit) and at configs[2]: kernel time of
 # the TSG_JIT_DIAG code variants (tsg_jit.cpp; diagnostic, results WRONG, the

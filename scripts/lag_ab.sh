@@ -1,4 +1,6 @@
 #!/bin/bash
+# TSG_JIT_DIAG code variants exist only in the diagnostic build (make -C ternary-spgemm_amd diag)
+export TSG_LIB=${TSG_LIB:-ternary-spgemm_amd/lib/libternary_spgemm_diag.so}
 # GPU box: is the weight-compiled kernel's step waiting on the LDS-DMA's
 # latency or paying for its issue?  Kernel ms (configs.py) of configs[1], M = 64
 # and 256 (K = 4096, N = 16384, the weight-compiled kernel forced), configs[2]

@@ -1,4 +1,6 @@
 #!/bin/bash
+# TSG_JIT_DIAG code variants exist only in the diagnostic build (make -C ternary-spgemm_amd diag)
+export TSG_LIB=${TSG_LIB:-ternary-spgemm_amd/lib/libternary_spgemm_diag.so}
 # GPU box, round 3 probe: LDS-DMA offset semantics micro-test, the launcher's
 # RCCL failure path on a 1-GPU box, kernel-time diagnostics (TSG_JIT_DIAG code
 # variants, results WRONG) at the sparse end (configs[3] s=16, s=8) and at

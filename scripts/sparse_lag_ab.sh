@@ -1,4 +1,6 @@
 #!/bin/bash
+# TSG_JIT_DIAG code variants exist only in the diagnostic build (make -C ternary-spgemm_amd diag)
+export TSG_LIB=${TSG_LIB:-ternary-spgemm_amd/lib/libternary_spgemm_diag.so}
 # GPU box: does the sparse end wait on the LDS-DMA's latency?  configs[3] at
 # s = 8 and 16: default, the pieces never waited for (TSG_JIT_DIAG=novm,
 # results WRONG, timing only), lag 2, no DMA (nodma, WRONG).  Kernel ms

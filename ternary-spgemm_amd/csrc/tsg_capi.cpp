@@ -14,7 +14,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/ternary_spgemm.h"
+#include "../../include/ternary_spgemm_test.h"
 #include "tsg_internal.h"
 
 extern thread_local std::string g_tsg_host_err;  // one per-thread message for the whole ABI
@@ -247,7 +247,7 @@ int shape_index(const JitShape &sh) { return shape_index(sh.nw, sh.waves, sh.far
 // slower; those run the 4 x 8 map).  TSG_JIT_FAR=0/1 overrides.
 bool far_xt(const tsg_tcsc *h, int M)
 {
-    static const int env = [] { const char *e = getenv("TSG_JIT_FAR"); return e ? atoi(e) : -1; }();
+    static const int env = [] { const char *e = tsg::knob_value("TSG_JIT_FAR"); return e ? atoi(e) : -1; }();
     if (h->B || h->far_mode == 1) return false;
     if (h->far_mode == 2) return true;
     if (h->jit_force) return false;
@@ -262,7 +262,7 @@ bool far_xt(const tsg_tcsc *h, int M)
 JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 {
     static const int env_waves = [] {
-        const char *e = getenv("TSG_JIT_WAVES");
+        const char *e = tsg::knob_value("TSG_JIT_WAVES");
         return e ? atoi(e) : 0;
     }();
     if (h->B) return {tsg::kJitNW, tsg::kJitWaves};
@@ -325,9 +325,9 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
 // TSG_JIT_GN / TSG_JIT_GM / TSG_JIT_TMASK override (A/B).
 void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, int &tmask)
 {
-    static const int env_gn = [] { const char *e = getenv("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
-    static const int env_gm = [] { const char *e = getenv("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
-    static const int env_tm = [] { const char *e = getenv("TSG_JIT_TMASK"); return e ? atoi(e) : -1; }();
+    static const int env_gn = [] { const char *e = tsg::knob_value("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
+    static const int env_gm = [] { const char *e = tsg::knob_value("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
+    static const int env_tm = [] { const char *e = tsg::knob_value("TSG_JIT_TMASK"); return e ? atoi(e) : -1; }();
     tmask = env_tm >= 0 ? env_tm : ((int64_t)mtiles * ntiles <= kJitOneRoundWgs && mtiles >= 4 ? 3 : 0);
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
     int n = 2, m = 16;
@@ -372,8 +372,9 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
     if ((uint64_t)img.code.size() * 4 >= (1ull << 32) - (1ull << 20))
         return fail(TSG_ERR_RANGE, "jit image of " + std::to_string((uint64_t)img.code.size() * 4) +
                                        " B exceeds the 32-bit stream offsets; shard W's columns");
+#ifdef TSG_DIAG
     if (nw == tsg::kJitNW && waves == tsg::kJitWaves)
-        if (const char *d = std::getenv("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
+        if (const char *d = tsg::knob_value("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
             const size_t S = tsg::kJitStreams;
             if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
                 for (size_t k = S; k < img.wcode.size(); k++) img.wcode[k] = img.wcode[k % S];
@@ -382,6 +383,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
             if (std::strstr(d, "pairwave"))  // waves 2i and 2i+1 share a stream
                 for (size_t k = 0; k < img.wcode.size(); k++) img.wcode[k] = img.wcode[k & ~(size_t)1];
         }
+#endif
     DeviceGuard g(h->device);
     const std::string err = v.mod.load(img.code, nw, waves);
     if (!err.empty()) return fail(TSG_ERR_HIP, "jit kernel (width " + std::to_string(nw) + "): " + err);
@@ -443,7 +445,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
 bool ell_pc_available(const tsg_tcsc *h)
 {
     static const bool on = [] {
-        const char *e = getenv("TSG_ELL_PC");
+        const char *e = tsg::knob_value("TSG_ELL_PC");
         return !(e && e[0] == '0');
     }();
     if (!on || h->small_m == 3 || h->K > tsg::kEllMaxC[0]) return false;
@@ -477,7 +479,7 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
                             ((h->N + 8 * tsg::kJitWaves - 1) / (8 * tsg::kJitWaves));
     const bool starved = M <= kEllStarvedMaxM && jit_wgs <= kEllStarvedWgs;
     static const int auto_max = [] {  // TSG_ELL_MAXM: A/B of the small-M boundary
-        const char *e = getenv("TSG_ELL_MAXM");
+        const char *e = tsg::knob_value("TSG_ELL_MAXM");
         return e ? atoi(e) : kEllAutoMaxM;
     }();
     if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) && !starved) return -1;
@@ -495,12 +497,12 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // small (M = 2 at N = 16384: 20.0 vs 22.9 us; M = 4 at N = 4096: 14.7 vs
     // 21.9 us; profiles/r02z2_pc_rows.txt)
     static const int64_t pc_rows_max_mn = [] {  // TSG_ELL_PC_MAXMN: A/B sweeps of the threshold
-        const char *e = getenv("TSG_ELL_PC_MAXMN");
+        const char *e = tsg::knob_value("TSG_ELL_PC_MAXMN");
         return e ? (int64_t)atoll(e) : kEllPcRowsMaxMN;
     }();
     if (M <= 4 && (int64_t)M * h->N <= pc_rows_max_mn && ell_pc_available(h)) v = 0;
     static const int force = [] {  // TSG_ELL_VARIANT: diagnostic sweeps only
-        const char *e = getenv("TSG_ELL_VARIANT");
+        const char *e = tsg::knob_value("TSG_ELL_VARIANT");
         return e ? atoi(e) : -1;
     }();
     if (force >= 0 && force < tsg::kEllVariants) v = force;
@@ -848,6 +850,10 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     if (!out) return fail(TSG_ERR_ARG, "null out");
     *out = nullptr;
     if (B < 0) return fail(TSG_ERR_ARG, "negative block size");
+    // a malformed environment knob (or, in the product build, the wrong-result
+    // diagnostics of TSG_JIT_DIAG) is refused before anything else
+    const std::string ke = tsg::knob_check();
+    if (!ke.empty()) return fail(TSG_ERR_ARG, ke);
     std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, B);
     if (!e.empty()) return fail(TSG_ERR_ARG, std::string(B ? "malformed BlockedTCSC: " : "malformed TCSC: ") + e);
     if (B && (tsg::kJitXRegs - tsg::kJitNW) / tsg::kJitSlotRegs < 2)
@@ -873,7 +879,7 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     if (h->nnz_neg) h->rin.assign(rin, rin + h->nnz_neg);
     // kernel family (default: the weight-compiled kernel); TSG_KERNEL selects
     // the others for A/B and their own tests
-    const char *kenv = std::getenv("TSG_KERNEL");
+    const char *kenv = tsg::knob_value("TSG_KERNEL");
     // The weight-compiled image costs ~8 B per nonzero plus ~15% schedule code;
     // stream offsets are 32-bit, so a W whose image would pass ~3 GiB (e.g.
     // K=16384, N=131072, s=4 on ONE GPU -- shard columns instead)
@@ -903,7 +909,7 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     h->kind = kname == "jit" ? tsg_tcsc::kJit : tsg_tcsc::kRx;
     if (h->kind == tsg_tcsc::kJit) {
         // TSG_JIT_NW=<64|32|16|8> pins the stream width (A/B); default: per call
-        if (const char *wv = std::getenv("TSG_JIT_NW")) {
+        if (const char *wv = tsg::knob_value("TSG_JIT_NW")) {
             const int nw = std::atoi(wv);
             if (width_index(nw) < 0 || !tsg::jit_width_ok(nw) || (B && nw != tsg::kJitNW)) {
                 free_handle(h);

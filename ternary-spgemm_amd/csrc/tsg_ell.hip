@@ -536,7 +536,7 @@ int launch_ell_la(const float *X, const uint4 *ent, const uint2 *tab, const floa
 int pick_la()
 {
     static const int env = [] {
-        const char *v = getenv("TSG_ELL_LA");
+        const char *v = knob_value("TSG_ELL_LA");
         const int x = v ? atoi(v) : 0;
         return x == 1 || x == 2 ? x : 0;
     }();
@@ -579,7 +579,7 @@ int launch_lg(const float *X, const uint4 *e, const uint2 *t, const float *b, co
 int pick_lg(int dflt)
 {
     static const int env = [] {
-        const char *v = getenv("TSG_ELL_LG");
+        const char *v = knob_value("TSG_ELL_LG");
         return v ? atoi(v) : 0;
     }();
     return env > 0 ? env : dflt;
@@ -626,7 +626,7 @@ namespace {
 int pc_phase(int M, int N, int C)
 {
     static const int env = [] {
-        const char *v = getenv("TSG_ELL_PC_E");
+        const char *v = knob_value("TSG_ELL_PC_E");
         const int x = v ? atoi(v) : 0;
         return x == 16 || x == 32 || x == 64 ? x : 0;
     }();

@@ -8,7 +8,7 @@
 #include <string>
 #include <vector>
 
-#include "../../include/ternary_spgemm.h"
+#include "../../include/ternary_spgemm_test.h"
 #include "tsg_internal.h"
 
 namespace tsg {

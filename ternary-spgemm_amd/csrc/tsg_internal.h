@@ -109,6 +109,9 @@ inline bool jit_width_ok(int nw) { return nw == kJitNW || nw == 32 || nw == 16 |
 // columns per workgroup -> twice the workgroups at mid M
 inline bool jit_waves_ok(int nw, int waves) { return waves == kJitWaves || (waves == 4 && nw != kJitNW); }
 
+// words of padding after the last stream (the code prefetch reads ahead)
+constexpr int kJitTailPadWords = 32768 + 1024;
+
 struct JitImage {
     int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0, waves = kJitWaves;
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
@@ -162,6 +165,16 @@ constexpr size_t kLdsBytes = 160 * 1024;
 size_t ell_pc_lds_bytes(int variant, int C);
 int launch_tcsc_ell_pc(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
                        const float *alpha, float *Y, int M, int N, int K, int C, int nch, int prelu, void *stream);
+
+// Environment knobs (csrc/tsg_knobs.cpp): A/B studies and tests, none of
+// which changes a result.  knob_check: "" when every set knob has an
+// accepted value, else the first error (registration and the host codegen
+// entry points refuse it); in the product build a set TSG_JIT_DIAG is an
+// error (its code variants give wrong results: diagnostic build only).
+// knob_value: the text of a set, valid knob, else nullptr.
+std::string knob_check();
+const char *knob_value(const char *name);
+bool diag_build();
 
 // B = 0: plain TCSC; B > 0: BlockedTCSC<B> arrays ((K/B)*N + 1 column starts)
 std::string validate_tcsc(const int32_t *csp, const int32_t *csn, const int32_t *rip,

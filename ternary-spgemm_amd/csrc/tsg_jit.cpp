@@ -25,7 +25,7 @@
 
 #include "tsg_internal.h"
 #include "tsg_jit_map.h"
-#include "../../include/ternary_spgemm.h"
+#include "../../include/ternary_spgemm_test.h"
 
 namespace tsg {
 
@@ -34,7 +34,7 @@ namespace {
 // --- gfx950 encodings (checked against llvm-mc -mcpu=gfx950 -show-encoding) ---
 struct Emit {
     std::vector<uint32_t> &c;
-    bool pad8 = std::getenv("TSG_JIT_NOALIGN") == nullptr;  // A/B knob (results unchanged)
+    bool pad8 = true;  // TSG_JIT_NOALIGN=1: A/B knob (results unchanged)
     // keep 8-byte instructions 8-byte aligned (hand-asm placement rule)
     void align8()
     {
@@ -145,7 +145,7 @@ struct JitRegs {
 static_assert(((kDmaOffV + kJitChunk / 2 / kJitWaves + 2) & ~1u) + 2 * kJitNW <= 256u, "VGPR budget");
 static_assert(((kDmaOffV + kJitChunk / 2 / 4 + 2) & ~1u) + 2 * 32 <= 256u, "VGPR budget, 4 waves");
 // narrower streams (jit width < kJitNW) use the same register contract, fewer accumulators
-constexpr int kTailPad = 32768 + 1024;   // words of padding after the last stream (code prefetch reads ahead)
+constexpr int kTailPad = kJitTailPadWords;  // words of padding after the last stream (code prefetch reads ahead)
 static_assert((kJitChunk / 2 - 1) * kPairBytes + 8 < 65536, "ds_read offset field");
 
 // One step's work for a wave: its X reads (k-row pairs of the chunk with an
@@ -252,7 +252,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // it, profiles/r03g_s2_ab.txt)
     double dma_spread = (K >= 8192 && density <= 0.1875) || (density > 0.375 && nw == kJitNW) ? 0.0 : 0.5;
     int m0k = 1, lag = 1;
-    if (const char *dv = std::getenv("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d,%d", &dma_spread, &m0k, &lag);
+    if (const char *dv = knob_value("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d,%d", &dma_spread, &m0k, &lag);
     if (lag != 2) lag = 1;
     // X slots: all of v[8 : 104) for BaseTCSC; BlockedTCSC keeps y of half the
     // columns (nw registers) at the top of that range
@@ -273,10 +273,11 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
                              (uint32_t)kJitRing | kJitFormat << 8 | (uint32_t)(m0k ? kJitM0kFlag : 0u) |
                                  (far ? kJitFarFlag : 0u)});
-    Emit E{code, std::getenv("TSG_JIT_NOALIGN") == nullptr};
+    const char *na = knob_value("TSG_JIT_NOALIGN");
+    Emit E{code, !(na && na[0] == '1')};
     // TSG_JIT_CP="dma,touch": cache-policy bits of the LDS-DMA pieces and the
     // code touches (hex; 0x20000 = nt, 0x2000000 = sc1, 0x10000 = sc0; A/B)
-    if (const char *cv = std::getenv("TSG_JIT_CP")) {
+    if (const char *cv = knob_value("TSG_JIT_CP")) {
         unsigned a = 0, t = 0;
         std::sscanf(cv, "%x,%x", &a, &t);
         E.dma_cp = a & 0x2030000u;
@@ -286,17 +287,23 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // stream does not evict the code from the Infinity Cache, and no code
     // touches
     if (far) E.dma_cp |= 0x20000u;
-    // TSG_JIT_DIAG: diagnostic code variants (results WRONG; timing studies only):
-    // comma list of nobar (no s_barrier), nodma (no LDS-DMA), notouch (no code
-    // prefetch), nolgkm (no LDS waits), noreads (no X reads), novm (the DMA
-    // pieces are never waited for: tells the DMA's latency from its issue cost)
-    const std::string diag = std::getenv("TSG_JIT_DIAG") ? std::getenv("TSG_JIT_DIAG") : "";
+    // TSG_JIT_DIAG (diagnostic build only, -DTSG_DIAG; results WRONG, timing
+    // studies): comma list of nobar (no s_barrier), nodma (no LDS-DMA),
+    // notouch (no code prefetch), nolgkm (no LDS waits), noreads (no X reads),
+    // novm (the DMA pieces are never waited for: tells the DMA's latency from
+    // its issue cost).  The product library never reads it (tsg_knobs.cpp).
+#ifdef TSG_DIAG
+    const std::string diag = knob_value("TSG_JIT_DIAG") ? knob_value("TSG_JIT_DIAG") : "";
     auto has = [&](const char *f) { return diag.find(f) != std::string::npos; };
     const bool d_nobar = has("nobar"), d_nodma = has("nodma"), d_notouch = has("notouch"),
                d_nolgkm = has("nolgkm"), d_noreads = has("noreads"), d_novm = has("novm");
+#else
+    constexpr bool d_nobar = false, d_nodma = false, d_notouch = false, d_nolgkm = false, d_noreads = false,
+                   d_novm = false;
+#endif
     // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,1)
     uint32_t touch_first = 1, touch_count = 1;
-    if (const char *tv = std::getenv("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
+    if (const char *tv = knob_value("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
     if (touch_count > 4) touch_count = 4;
     // the prefetch must stay inside the tail padding past the last stream
     if ((touch_first + touch_count) * 8192u > (uint32_t)kTailPad * 4u) touch_first = (uint32_t)kTailPad * 4u / 8192u - touch_count;
@@ -380,7 +387,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // Default G = S/3, RA = 2S/3 (8 and 16 of the 24 slots: measured 0.4% faster
     // than 12,12, profiles/r02_jit_knobs_ab.txt); TSG_JIT_READS="G,RA" overrides.
     int G = std::max(1, S / 3), RA = S - std::max(1, S / 3);
-    if (const char *rv = std::getenv("TSG_JIT_READS")) std::sscanf(rv, "%d,%d", &G, &RA);
+    if (const char *rv = knob_value("TSG_JIT_READS")) std::sscanf(rv, "%d,%d", &G, &RA);
     if (G < 1 || RA < 0 || G + RA > S) {
         G = std::max(1, S / 3);
         RA = S - G;
@@ -541,7 +548,7 @@ std::string template_path(int nw, int waves)
 {
     const std::string name = nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
                              : "tsg_jit_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co";
-    if (const char *dir = std::getenv("TSG_JIT_DIR")) return std::string(dir) + "/" + name;  // tests: rx fallback
+    if (const char *dir = knob_value("TSG_JIT_DIR")) return std::string(dir) + "/" + name;  // tests: rx fallback
     Dl_info info;
     if (dladdr(reinterpret_cast<void *>(&build_jit_code), &info) && info.dli_fname) {
         std::string p(info.dli_fname);
@@ -680,6 +687,11 @@ extern "C" int tsg_jit_codegen_wv(const int32_t *csp, const int32_t *csn, const 
         g_tsg_host_err = std::string(B ? "tsg_jit_codegen: malformed BlockedTCSC: " : "tsg_jit_codegen: malformed TCSC: ") + e;
         return TSG_ERR_ARG;
     }
+    const std::string ke = tsg::knob_check();
+    if (!ke.empty()) {
+        g_tsg_host_err = "tsg_jit_codegen: " + ke;
+        return TSG_ERR_ARG;
+    }
     if (B && (tsg::kJitXRegs - tsg::kJitNW) / tsg::kJitSlotRegs < 2) {
         g_tsg_host_err = "tsg_jit_codegen: this kernel geometry has no registers for BlockedTCSC";
         return TSG_ERR_ARG;
@@ -704,6 +716,11 @@ extern "C" int tsg_jit_codegen_far(const int32_t *csp, const int32_t *csn, const
     const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, 0);
     if (!e.empty()) {
         g_tsg_host_err = "tsg_jit_codegen_far: malformed TCSC: " + e;
+        return TSG_ERR_ARG;
+    }
+    const std::string ke = tsg::knob_check();
+    if (!ke.empty()) {
+        g_tsg_host_err = "tsg_jit_codegen_far: " + ke;
         return TSG_ERR_ARG;
     }
     tsg::JitImage img;

@@ -31,7 +31,9 @@ TSG_OK = 0
 _ERRNAMES = {1: "TSG_ERR_ARG", 2: "TSG_ERR_HIP", 3: "TSG_ERR_NOMEM", 4: "TSG_ERR_NODEV",
              5: "TSG_ERR_RANGE"}
 
-# Every symbol include/ternary_spgemm.h declares (tests check the .so exports them).
+# Every symbol include/ternary_spgemm.h (the drop-in surface) and
+# include/ternary_spgemm_test.h (tuning and test hooks) declare; tests check
+# the .so exports them.
 EXPORTED_SYMBOLS = (
     "tcsc_hip_create", "tcsc_hip_create_dense", "tcsc_hip_destroy", "tcsc_hip_gemm",
     "tcsc_hip_gemm_dev", "tcsc_hip_gemm_prelu", "tcsc_hip_gemm_prelu_dev", "tcsc_hip_reserve",
@@ -44,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
     "tcsc_hip_host_register", "tcsc_hip_host_unregister", "tcsc_hip_set_far", "tcsc_hip_call_far",
-    "tsg_jit_codegen_far", "tsg_call_plan",
+    "tsg_jit_codegen_far", "tsg_call_plan", "tsg_knob_check",
 )
 
 
@@ -139,6 +141,8 @@ def lib() -> C.CDLL:
     L.tcsc_hip_host_unregister.argtypes = [vp]
     L.tcsc_hip_call_kernel.argtypes = [H, C.c_int]
     L.tcsc_hip_call_kernel.restype = C.c_char_p
+    L.tsg_knob_check.argtypes = []
+    L.tsg_knob_check.restype = C.c_char_p
     L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
                                 vp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     L.tsg_jit_tile_map.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -147,11 +151,17 @@ def lib() -> C.CDLL:
     L.tcsc_hip_set_jit_width.argtypes = [H, C.c_int]
     for f in EXPORTED_SYMBOLS:
         if f not in ("tcsc_hip_destroy", "tcsc_hip_last_error", "tcsc_hip_kernel_name", "tcsc_hip_call_kernel",
-                     "tcsc_hip_call_image_bytes"):
+                     "tcsc_hip_call_image_bytes", "tsg_knob_check"):
             getattr(L, f).restype = C.c_int
     L.tcsc_hip_call_image_bytes.restype = C.c_int64
     _LIB = L
     return L
+
+
+def knob_check() -> str:
+    """"" when every set TSG_* environment knob has an accepted value, else
+    the error registration reports (include/ternary_spgemm_test.h)."""
+    return lib().tsg_knob_check().decode()
 
 
 def _check(rc: int, where: str) -> None:

@@ -12,10 +12,12 @@ import pytest
 from conftest import REPO, gpu_available
 
 
-def _declared_functions():
-    text = open(os.path.join(REPO, "include", "ternary_spgemm.h")).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    names = re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(t\w+)\s*\(", text, flags=re.M)
+def _declared_functions(headers=("ternary_spgemm.h", "ternary_spgemm_test.h")):
+    names = []
+    for hdr in headers:
+        text = open(os.path.join(REPO, "include", hdr)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(t\w+)\s*\(", text, flags=re.M)
     return sorted(set(names))
 
 
@@ -142,3 +144,72 @@ def test_tcsc_to_blocked_matches_blocked_ctor(tsg, oracle_mod, K, N, s, B):
     for g, w in zip(got, want):
         assert np.array_equal(np.asarray(g, np.int32), np.asarray(w, np.int32))
     tsg.validate_blocked(*got, K, N, B)
+
+
+def test_drop_in_header_is_the_product_surface():
+    """include/ternary_spgemm.h carries the drop-in surface only; the tuning
+    and test hooks live in ternary_spgemm_test.h (both exported by the .so)."""
+    product = set(_declared_functions(("ternary_spgemm.h",)))
+    hooks = set(_declared_functions(("ternary_spgemm_test.h",)))
+    assert not product & hooks
+    for f in ("tcsc_hip_create", "tcsc_hip_gemm", "tcsc_hip_gemm_dev", "tcsc_hip_gemm_prelu", "tcsc_hip_destroy",
+              "tcsc_hip_reserve", "tcsc_hip_last_error"):
+        assert f in product
+    for f in ("tcsc_hip_set_jit_width", "tcsc_hip_set_small_m", "tcsc_hip_set_far", "tsg_jit_codegen_wv",
+              "tsg_call_plan", "tsg_jit_tile_map", "tsg_ell_build", "tsg_knob_check"):
+        assert f in hooks
+
+
+def _small_tcsc(oracle_mod):
+    t = oracle_mod.tcsc_encode(oracle_mod.gen_ternary(64, 32, 4, 3))
+    return t.arrays, 64, 32
+
+
+@pytest.mark.parametrize("var,val,msg", [
+    ("TSG_JIT_DIAG", "nodma", "WRONG results"),          # wrong-result diagnostics: diagnostic build only
+    ("TSG_JIT_DIAG", "nobar,noreads", "WRONG results"),
+    ("TSG_JIT_DMA", "0.5;1", "TSG_JIT_DMA=0.5;1: expected"),
+    ("TSG_JIT_DMA", "2,1", "expected"),                  # spread outside [0, 1]
+    ("TSG_JIT_TOUCH", "1,9", "expected"),
+    ("TSG_JIT_READS", "20,20", "expected"),
+    ("TSG_JIT_CP", "0x40,0", "expected"),
+    ("TSG_JIT_GN", "two", "expected"),
+    ("TSG_JIT_NOALIGN", "yes", "expected"),
+    ("TSG_KERNEL", "fast", "expected"),
+    ("TSG_ELL_VARIANT", "7", "expected"),
+])
+def test_registration_refuses_bad_knobs(tsg, oracle_mod, monkeypatch, var, val, msg):
+    """A set knob outside its accepted values -- and, in the product library,
+    TSG_JIT_DIAG at all -- fails registration with TSG_ERR_ARG before any
+    device is touched (so this runs on the CPU), and the host codegen refuses
+    it too; nothing is parsed leniently."""
+    arrays, K, N = _small_tcsc(oracle_mod)
+    monkeypatch.setenv(var, val)
+    assert msg in tsg.knob_check()
+    with pytest.raises(tsg.TSGError, match="TSG_ERR_ARG") as e:
+        tsg.TCSCDevice(*arrays, K, N)
+    assert var in str(e.value)
+    with pytest.raises(tsg.TSGError, match=var):
+        tsg.jit_codegen(*arrays, K, N)
+
+
+@pytest.mark.parametrize("var,val", [
+    ("TSG_JIT_DMA", "0.25,1"), ("TSG_JIT_DMA", "0,0,2"), ("TSG_JIT_TOUCH", "1,2"), ("TSG_JIT_READS", "6,12"),
+    ("TSG_JIT_CP", "20000,0"), ("TSG_JIT_NOALIGN", "1"), ("TSG_KERNEL", "rx"), ("TSG_ELL_LG", "8"),
+])
+def test_accepted_knobs_pass(tsg, monkeypatch, var, val):
+    monkeypatch.setenv(var, val)
+    assert tsg.knob_check() == ""
+
+
+def test_diag_build_accepts_diag_variants(monkeypatch):
+    """The diagnostic build (make diag) is the only one that takes TSG_JIT_DIAG."""
+    path = os.path.join(REPO, "ternary-spgemm_amd", "lib", "libternary_spgemm_diag.so")
+    if not os.path.exists(path):
+        pytest.skip("diagnostic build not present (make -C ternary-spgemm_amd diag)")
+    L = ctypes.CDLL(path)
+    L.tsg_knob_check.restype = ctypes.c_char_p
+    monkeypatch.setenv("TSG_JIT_DIAG", "nodma,novm")
+    assert L.tsg_knob_check() == b""
+    monkeypatch.setenv("TSG_JIT_DIAG", "nodma,typo")
+    assert b"expected" in L.tsg_knob_check()
