@@ -405,8 +405,12 @@ def main():
         e_ms, e_ok = host_ms(0)  # the default: M-chunk pipeline
         with T.registered_host(Xh, Yh):  # the caller's buffers page-locked once (tcsc_hip_host_register)
             reg_ms, reg_ok = host_ms(0)
+        rows = h.host_chunk_rows(M)
         e2e = {"ms": round(e_ms, 3), "gflops": round(T.flops(M, Nr, nnz) / (e_ms * 1e-3) / 1e9, 1),
-               "chunk_rows": h.host_chunk_rows(M), "unpipelined_ms": round(serial_ms, 3),
+               "chunk_rows": rows, "unpipelined_ms": round(serial_ms, 3),
+               # what each chunk runs: the per-call plan of a call with `rows` rows
+               "chunk_plan": {"kernel": h.call_kernel(rows), "width": h.jit_width(rows),
+                              "waves": h.jit_waves(rows), "far": h.call_far(rows)},
                "registered_buffers_ms": round(reg_ms, 3),
                "bit_identical_to_device_call": e_ok and serial_ok and reg_ok, "timing": "median of 5 calls",
                "bytes_over_pcie": 4 * (M * K + Nr + M * Nr)}

@@ -346,9 +346,12 @@ void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, i
     gm = std::min(env_gm > 0 ? env_gm : m, std::max(mtiles, 1));
 }
 
+// The handle's own non-blocking stream (host-pointer calls, probes without a
+// call stream): created once at registration (create_impl), so threads never
+// race to create it.
 int handle_stream(tsg_tcsc *h, hipStream_t &s)
 {
-    if (!h->stream) HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    if (!h->stream) return fail(TSG_ERR_HIP, "handle has no stream (registration did not complete)");
     s = h->stream;
     return TSG_OK;
 }
@@ -690,8 +693,25 @@ int host_pipe_ready(tsg_tcsc *h)
 // chunk's compute), so the H2D of chunk i+1, the kernel of chunk i and the
 // D2H of chunk i-1 overlap (PCIe is full duplex).  Rows are independent, so
 // the chunked result is the unchunked one bit for bit.
-int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, float *Y, int M,
-             int N, int K, bool prelu)
+int run_host_impl(tsg_tcsc *h, const float *X, const float *b, const float *alpha, float *Y, int M, int N, int K,
+                  bool prelu);
+
+// No exception crosses the extern "C" boundary: a std::bad_alloc or
+// std::system_error (thread creation) inside the pipeline becomes a status.
+int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, float *Y, int M, int N, int K,
+             bool prelu)
+{
+    try {
+        return run_host_impl(h, X, b, alpha, Y, M, N, K, prelu);
+    } catch (const std::bad_alloc &) {
+        return fail(TSG_ERR_NOMEM, "host-pointer call: out of host memory");
+    } catch (const std::exception &e) {
+        return fail(TSG_ERR_HIP, std::string("host-pointer call: ") + e.what());
+    }
+}
+
+int run_host_impl(tsg_tcsc *h, const float *X, const float *b, const float *alpha, float *Y, int M, int N, int K,
+                  bool prelu)
 {
     if (!h) return fail(TSG_ERR_ARG, "null handle");
     if (N != h->N || K != h->K) return run_dev(h, nullptr, nullptr, nullptr, nullptr, M, N, K, nullptr, prelu);
@@ -739,6 +759,23 @@ int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, fl
     std::condition_variable cv;
     int enq = 0;
     hipError_t out_err = hipSuccess;
+    // joins the helper on every path out of this scope (an exception included)
+    struct Joiner {
+        std::thread &t;
+        std::mutex &m;
+        std::condition_variable &cv;
+        int &enq;
+        ~Joiner()
+        {
+            if (!t.joinable()) return;
+            {
+                std::lock_guard<std::mutex> gl(m);
+                enq = -1;
+            }
+            cv.notify_all();
+            t.join();
+        }
+    };
     std::thread out([&] {
         DeviceGuard tg(h->device);
         for (int i = 0; i < nchunk && out_err == hipSuccess; i++) {
@@ -756,6 +793,7 @@ int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, fl
         const hipError_t e = hipStreamSynchronize(h->s_out);
         if (out_err == hipSuccess) out_err = e;
     });
+    Joiner joiner{out, m, cv, enq};
     auto stop = [&](int code) {
         {
             std::lock_guard<std::mutex> gl(m);
@@ -786,7 +824,12 @@ int run_host(tsg_tcsc *h, const float *X, const float *b, const float *alpha, fl
         cv.notify_all();
     }
     stop(0);
-    if (out_err != hipSuccess) return fail(TSG_ERR_HIP, std::string("host pipeline (Y chunk): ") + hipGetErrorString(out_err));
+    if (out_err != hipSuccess) {
+        // chunks still queued on the compute stream may read d_x / write d_y:
+        // drain them before the next call's copies can overwrite d_x
+        (void)hipStreamSynchronize(s);
+        return fail(TSG_ERR_HIP, std::string("host pipeline (Y chunk): ") + hipGetErrorString(out_err));
+    }
     HIP_TRY(hipStreamSynchronize(s));
     return TSG_OK;
 }
@@ -871,6 +914,13 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     h->N = N;
     h->B = B;
     h->device = device;
+    {
+        DeviceGuard g0(device);
+        if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete h;
+            return fail(TSG_ERR_HIP, "hipStreamCreate of the handle's stream failed");
+        }
+    }
     h->nnz_pos = csp[slots];
     h->nnz_neg = csn[slots];
     h->csp.assign(csp, csp + slots + 1);

@@ -395,9 +395,17 @@ class registered_host:
             raise
         return self
 
-    def __exit__(self, *exc):
+    def __exit__(self, exc_type, exc, tb):
+        # unlock every array even if one fails; report a failure only when the
+        # with-block itself did not raise (never mask its exception)
+        errors = []
         for a in self.arrays:
-            _check(lib().tcsc_hip_host_unregister(a.ctypes.data), "tcsc_hip_host_unregister")
+            rc = lib().tcsc_hip_host_unregister(a.ctypes.data)
+            if rc != TSG_OK:
+                errors.append(TSGError(rc, "tcsc_hip_host_unregister", lib().tcsc_hip_last_error().decode(errors="replace")))
+        if errors and exc_type is None:
+            raise errors[0]
+        return False
 
 
 def device_count() -> int:
