@@ -126,6 +126,23 @@ int tsg_ell_build(const int32_t *col_start_pos, const int32_t *col_start_neg, co
                   const int32_t *row_index_neg, int K, int N, int Cmax, int MT, uint32_t *ent, int64_t ent_cap,
                   int64_t *ent_len, uint32_t *tab, int64_t tab_cap, int64_t *tab_len, int32_t *C, int32_t *nch);
 
+/* The 64-row image (no reference counterpart): one M row per
+ * lane, 64-row M tiles, every nonzero one 4-byte VOP2 v_add_f32 / v_sub_f32,
+ * X^T in the k-quad layout.  Same results bit for bit.  rows: 0 = automatic
+ * (default), 64 = the 64-row image, 128 = the 128-row image (v_pk_add_f32) for
+ * every weight-compiled call (plain TCSC only).  tcsc_hip_call_tile_rows: the
+ * M tile (64 / 128) of a call with M rows, 0 if it runs a small-M walk. */
+int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows);
+int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M);
+
+/* The 64-row image's machine code (layout as tsg_jit_codegen; region header
+ * word 7 format 3, the k-quad layout): width 64 / 32 / 16 / 8, waves 8 (or 4
+ * for the narrow widths). */
+int tsg_jit_codegen64(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                      const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                      int width, int waves, uint32_t *code, int64_t code_cap, int64_t *code_len,
+                      uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+
 /* The environment knobs (csrc/tsg_knobs.cpp): "" when every set TSG_* knob
  * has an accepted value, else the error registration reports (a set
  * TSG_JIT_DIAG is an error in the product build: its code variants give

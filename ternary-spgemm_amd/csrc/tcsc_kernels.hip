@@ -117,6 +117,50 @@ __global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *_
     }
 }
 
+// X [M][K] -> the k-quad layout of the 64-row image (tsg_internal.h):
+// XQ[(q * Mp + m) * 4 + j] = X[m][4q + j], zero past M or K.  A 64 x 64 tile
+// of X is read along k (coalesced rows) into LDS, then written as 16 quad
+// rows of 64 float4 (1 KiB each, coalesced).
+template <bool VEC>
+__global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *__restrict__ X,
+                                                                  float *__restrict__ XQ, int M, int K,
+                                                                  int Mp, int Kp)
+{
+    __shared__ float tile[64][65];  // [m][k]
+    const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+    if (VEC) {
+        const int c4 = (threadIdx.x & 15) * 4, r = threadIdx.x >> 4;  // 16 x 16
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int ml = r + 16 * i, m = m0 + ml, k = k0 + c4;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (m < M && k < K) v = *reinterpret_cast<const float4 *>(X + (size_t)m * K + k);  // K % 4 == 0
+            tile[ml][c4] = v.x;
+            tile[ml][c4 + 1] = v.y;
+            tile[ml][c4 + 2] = v.z;
+            tile[ml][c4 + 3] = v.w;
+        }
+    } else {
+        const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int m = m0 + ty + 4 * i, k = k0 + tx;
+            tile[ty + 4 * i][tx] = (m < M && k < K) ? X[(size_t)m * K + k] : 0.0f;
+        }
+    }
+    __syncthreads();
+    // 16 quads x 64 M rows of float4 per tile: 4 per thread, lane = M row
+    const int ml = threadIdx.x & 63, ql0 = threadIdx.x >> 6;  // 64 x 4
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int ql = ql0 + 4 * i, q = (k0 >> 2) + ql;
+        if (4 * q >= Kp) continue;
+        const int kk = 4 * ql;
+        *reinterpret_cast<float4 *>(XQ + ((size_t)q * Mp + (size_t)m0 + ml) * 4) =
+            make_float4(tile[ml][kk], tile[ml][kk + 1], tile[ml][kk + 2], tile[ml][kk + 3]);
+    }
+}
+
 // One LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS
 // [lds_dst, lds_dst + 1 KiB).  Inline asm on purpose: hipcc cannot prove that
 // later ds_reads do not alias an in-flight LDS-DMA and would put
@@ -281,6 +325,21 @@ int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int 
                            Mp, Kp);
     else
         hipLaunchKernelGGL(tsg_transpose_pairs_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, X, XP, M, K,
+                           Mp, Kp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, void *stream)
+{
+    // Mp is a multiple of 64 (the 64-row image's M tile) and Kp of 192: the
+    // 64 x 64 tiles cover [0, Kp) x [0, Mp) exactly
+    if (Mp % 64 || Kp % 64) return -1;
+    dim3 grid((unsigned)(Kp / 64), (unsigned)(Mp / 64));
+    if (K % 4 == 0 && ((uintptr_t)X & 15) == 0)
+        hipLaunchKernelGGL(tsg_transpose_quads_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, X, XQ, M, K,
+                           Mp, Kp);
+    else
+        hipLaunchKernelGGL(tsg_transpose_quads_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, X, XQ, M, K,
                            Mp, Kp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

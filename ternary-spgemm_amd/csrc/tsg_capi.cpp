@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <atomic>
+#include <iterator>
 #include <condition_variable>
 #include <mutex>
 #include <string>
@@ -51,7 +52,10 @@ struct tsg_tcsc {
         int64_t code_bytes = 0, wcode_words = 0;
     };
     JitVariant jv[8];                     // 7: the 64 x 8 "far X^T" image (pick_jit_shape)
+    JitVariant jv64[7];                   // the 64-row image (tsg_internal.h), shape_index 0..6
     int jit_nch = 0;                      // X^T chunks (all widths)
+    int jit64_nch = 0;                    // X^T chunks of the 64-row image (192 rows each)
+    int tile_rows = 0;                    // tcsc_hip_set_tile_rows: 0 auto, 128 or 64 (jit images)
     int jit_force = 0;                    // tcsc_hip_set_jit_width / TSG_JIT_NW: 0 = auto
     uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
     // small-M kernel (tsg_ell.hip): one sliced-ELL image per variant, built on
@@ -138,22 +142,25 @@ int check_device(int dev)
     return TSG_OK;
 }
 
-int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp)
+// X^T dimensions of a call with M rows: rows padded to the M tile, K to
+// whole chunks (64-row image: k-quad layout, 64-row tiles, 192-row chunks)
+int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp, bool r64 = false)
 {
     const bool jit = h->kind == tsg_tcsc::kJit;
-    const int tm = jit ? tsg::kJitTileM : tsg::kRxTileM;
+    const int tm = !jit ? tsg::kRxTileM : r64 ? tsg::kJit64TileM : tsg::kJitTileM;
     Mp = ((std::max(M, 1) + tm - 1) / tm) * tm;
-    Kp = jit ? h->jit_nch * tsg::kJitChunk : h->rimg.nch * tsg::kRxChunk;
+    const int nch64 = std::max(1, (h->K + tsg::kJit64Chunk - 1) / tsg::kJit64Chunk);
+    Kp = !jit ? h->rimg.nch * tsg::kRxChunk : r64 ? nch64 * tsg::kJit64Chunk : h->jit_nch * tsg::kJitChunk;
     return TSG_OK;
 }
 
 // Grows the X^T work buffer (grow-only).  A grow frees the old buffer, so it
 // first waits for every launch that may still read it; it cannot happen while
 // a stream is being captured (tcsc_hip_reserve(max_M) before the capture).
-int ensure_work(tsg_tcsc *h, int M, bool capturing)
+int ensure_work(tsg_tcsc *h, int M, bool capturing, bool r64 = false)
 {
     int Mp, Kp;
-    dims_for(h, M, Mp, Kp);
+    dims_for(h, M, Mp, Kp, r64);
     const size_t need = (size_t)Mp * Kp * sizeof(float);
     if (need <= h->work_bytes) return TSG_OK;
     if (capturing)
@@ -218,8 +225,14 @@ int shape_index(int nw, int waves, bool far = false)
 struct JitShape {
     int nw, waves;
     bool far = false;  // the far-X^T code image (tsg_jit.cpp build_jit_code)
+    bool r64 = false;  // the 64-row image (tsg_internal.h)
 };
-int shape_index(const JitShape &sh) { return shape_index(sh.nw, sh.waves, sh.far); }
+int shape_index(const JitShape &sh) { return shape_index(sh.nw, sh.waves, sh.far && !sh.r64); }
+
+tsg_tcsc::JitVariant &variant_of(tsg_tcsc *h, const JitShape &sh)
+{
+    return sh.r64 ? h->jv64[shape_index(sh.nw, sh.waves)] : h->jv[shape_index(sh)];
+}
 
 // Shape (stream width x waves per workgroup) for a call with M rows.  Every
 // shape walks the same X^T chunks; a wider stream reads fewer LDS bytes per
@@ -259,7 +272,17 @@ bool far_xt(const tsg_tcsc *h, int M)
     return long_map && 4.0 * (double)M * (double)h->K >= kFarXtBytes && 8.0 * nnz <= kFarCodeBytes;
 }
 
-JitShape pick_jit_shape(const tsg_tcsc *h, int M)
+// The 64-row image (VOP2 adds, one M row per lane) or the 128-row one
+// (v_pk_add_f32, two rows per lane) for a call with M rows; BlockedTCSC runs
+// the 128-row image only.  tcsc_hip_set_tile_rows pins one.
+bool pick_rows64(const tsg_tcsc *h, int M)
+{
+    (void)M;
+    if (h->B || h->kind != tsg_tcsc::kJit) return false;
+    return h->tile_rows == 64;
+}
+
+JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64 = false)
 {
     static const int env_waves = [] {
         const char *e = tsg::knob_value("TSG_JIT_WAVES");
@@ -268,10 +291,11 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
     if (h->B) return {tsg::kJitNW, tsg::kJitWaves};
     if (h->jit_force) {
         const int w = env_waves == 4 && tsg::jit_waves_ok(h->jit_force, 4) ? 4 : tsg::kJitWaves;
-        return {h->jit_force, w, h->jit_force == tsg::kJitNW && w == tsg::kJitWaves && far_xt(h, M)};
+        return {h->jit_force, w, !r64 && h->jit_force == tsg::kJitNW && w == tsg::kJitWaves && far_xt(h, M), r64};
     }
-    const int64_t mt = (std::max(M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM;
-    const double image8 = 8.0 * (double)(h->nnz_pos + h->nnz_neg);
+    const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM;
+    const int64_t mt = (std::max(M, 1) + tile_m - 1) / tile_m;
+    const double image8 = (r64 ? 4.0 : 8.0) * (double)(h->nnz_pos + h->nnz_neg);
     JitShape best{tsg::kJitNW, tsg::kJitWaves}, most{tsg::kJitNW, tsg::kJitWaves};
     int64_t most_wgs = -1;
     bool full = false;
@@ -295,7 +319,8 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M)
         }
     }
     JitShape sh = full ? best : most;
-    sh.far = sh.nw == tsg::kJitNW && sh.waves == tsg::kJitWaves && far_xt(h, M);
+    sh.far = !r64 && sh.nw == tsg::kJitNW && sh.waves == tsg::kJitWaves && far_xt(h, M);
+    sh.r64 = r64;
     return sh;
 }
 
@@ -360,23 +385,24 @@ int handle_stream(tsg_tcsc *h, hipStream_t &s)
 // or the first call that picks it) and runs its probe on `s` -- the call's
 // stream, or the handle's own non-blocking stream (nullptr) -- and
 // synchronises that stream only.  Caller holds h->mu (or owns h exclusively).
-int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStream_t s = nullptr, bool far = false)
+int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStream_t s = nullptr, bool far = false,
+                       bool r64 = false)
 {
-    const int i = shape_index(nw, waves, far);
-    if (i < 0 || !tsg::jit_width_ok(nw))
+    const int i = shape_index(nw, waves, far && !r64);
+    if (i < 0 || !tsg::jit_width_ok(nw) || (r64 && (far || h->B)))
         return fail(TSG_ERR_ARG, "unsupported jit stream width " + std::to_string(nw) + " x " + std::to_string(waves) +
-                                 " waves");
-    tsg_tcsc::JitVariant &v = h->jv[i];
+                                 " waves" + (r64 ? " (64-row image)" : ""));
+    tsg_tcsc::JitVariant &v = r64 ? h->jv64[i] : h->jv[i];
     if (v.mod.function) return TSG_OK;
     tsg::JitImage img;
     tsg::build_jit_code(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
-                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw, waves, far);
+                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw, waves, far, r64);
     // stream offsets (wcode) and the dispatcher's region literal are 32-bit
     if ((uint64_t)img.code.size() * 4 >= (1ull << 32) - (1ull << 20))
         return fail(TSG_ERR_RANGE, "jit image of " + std::to_string((uint64_t)img.code.size() * 4) +
                                        " B exceeds the 32-bit stream offsets; shard W's columns");
 #ifdef TSG_DIAG
-    if (nw == tsg::kJitNW && waves == tsg::kJitWaves)
+    if (nw == tsg::kJitNW && waves == tsg::kJitWaves && !r64)
         if (const char *d = tsg::knob_value("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
             const size_t S = tsg::kJitStreams;
             if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
@@ -388,7 +414,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
         }
 #endif
     DeviceGuard g(h->device);
-    const std::string err = v.mod.load(img.code, nw, waves);
+    const std::string err = v.mod.load(img.code, nw, waves, r64);
     if (!err.empty()) return fail(TSG_ERR_HIP, "jit kernel (width " + std::to_string(nw) + "): " + err);
     const size_t wb = img.wcode.size() * sizeof(uint32_t);
     if (hipMalloc(&v.d_wcode, std::max<size_t>(wb, 4)) != hipSuccess) {
@@ -436,7 +462,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
     v.Npad = img.Npad;
     v.code_bytes = (int64_t)img.code.size() * 4;
     v.wcode_words = (int64_t)img.wcode.size();
-    h->jit_nch = img.nch;
+    (r64 ? h->jit64_nch : h->jit_nch) = img.nch;
     return TSG_OK;
 }
 
@@ -593,23 +619,25 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         }
         return TSG_OK;
     }
-    rc = ensure_work(h, M, capturing);
+    const bool r64 = pick_rows64(h, M);
+    const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM, chunk = r64 ? tsg::kJit64Chunk : tsg::kJitChunk;
+    rc = ensure_work(h, M, capturing, r64);
     if (rc) return rc;
     int Mp, Kp;
-    dims_for(h, M, Mp, Kp);
+    dims_for(h, M, Mp, Kp, r64);
     tsg_tcsc::JitVariant *jv = nullptr;
     if (h->kind == tsg_tcsc::kJit) {
-        const JitShape sh = pick_jit_shape(h, M);
-        jv = &h->jv[shape_index(sh)];
+        const JitShape sh = pick_jit_shape(h, M, r64);
+        jv = &variant_of(h, sh);
         if (!jv->mod.function && capturing)
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(sh.nw) +
                                          " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
-        rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far);
+        rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far, r64);
         if (rc) return rc;
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
-        const int64_t wgs = (int64_t)(Mp / tsg::kJitTileM) * (jv->Npad / (jv->nw * jv->waves));
-        if ((int64_t)Mp * tsg::kJitChunk * 4 >= (1ll << 31) || wgs * jv->waves * 64 >= (1ll << 32))
+        const int64_t wgs = (int64_t)(Mp / tile_m) * (jv->Npad / (jv->nw * jv->waves));
+        if ((int64_t)Mp * chunk * 4 >= (1ll << 31) || wgs * jv->waves * 64 >= (1ll << 32))
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " is too large for one jit launch; split the rows");
     }
     // X^T of the previous call may still be read by its kernel on another
@@ -618,8 +646,9 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     if (K == 0) {
         // no X at all: chain is +0; X^T stays zero
         HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
-    } else if ((h->kind == tsg_tcsc::kJit ? tsg::launch_transpose_pairs(dX, h->d_work, M, K, Mp, Kp, s)
-                                          : tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s)) != 0) {
+    } else if ((h->kind != tsg_tcsc::kJit ? tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s)
+                : r64                      ? tsg::launch_transpose_quads(dX, h->d_work, M, K, Mp, Kp, s)
+                                           : tsg::launch_transpose_pairs(dX, h->d_work, M, K, Mp, Kp, s)) != 0) {
         return fail(TSG_ERR_HIP, std::string("transpose launch: ") + hipGetErrorString(hipGetLastError()));
     }
     int slot = -1;
@@ -631,10 +660,11 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     int gn = 2, gm = 16, tmask = 0;
     if (h->kind == tsg_tcsc::kJit)
-        pick_jit_map(h, Mp / tsg::kJitTileM, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask);
+        pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask);
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
-                               h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves, jv->waves, gn, gm, tmask, s)
+                               r64 ? h->jit64_nch : h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
+                               jv->waves, gn, gm, tmask, s, tile_m)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)
@@ -843,10 +873,11 @@ void free_handle(tsg_tcsc *h)
     for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_x,
                     (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha, (void *)h->d_status})
         if (p) (void)hipFree(p);
-    for (auto &v : h->jv) {
-        if (v.d_wcode) (void)hipFree(v.d_wcode);
-        v.mod.unload();
-    }
+    for (auto *vs : {&h->jv[0], &h->jv64[0]})
+        for (size_t i = 0; i < (vs == &h->jv[0] ? std::size(h->jv) : std::size(h->jv64)); i++) {
+            if (vs[i].d_wcode) (void)hipFree(vs[i].d_wcode);
+            vs[i].mod.unload();
+        }
     for (auto &e : h->ell) {
         if (e.d_ent) (void)hipFree(e.d_ent);
         if (e.d_tab) (void)hipFree(e.d_tab);
@@ -1110,15 +1141,20 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
     DeviceGuard g(h->device);
     std::lock_guard<std::mutex> lk(h->mu);
     int rc = ensure_work(h, max_M, false);
+    if (!rc) rc = ensure_work(h, max_M, false, true);  // the 64-row image's k-quad X^T (same bytes or fewer)
     if (rc || h->kind != tsg_tcsc::kJit) return rc;
-    const int mtiles = (std::max(max_M, 1) + tsg::kJitTileM - 1) / tsg::kJitTileM;
-    for (int mt = 1; mt <= mtiles; mt++) {
-        const int m = std::min(max_M, mt * tsg::kJitTileM);
-        if (pick_ell_variant(h, m) >= 0 && pick_ell_variant(h, std::min(m, (mt - 1) * tsg::kJitTileM + 1)) >= 0)
-            continue;  // every M of this tile runs the small-M kernel
-        const JitShape sh = pick_jit_shape(h, m);
-        rc = ensure_jit_variant(h, sh.nw, sh.waves, nullptr, sh.far);
-        if (rc) return rc;
+    // the image choice and its shape depend on M only through the 64- / 128-row
+    // M tiles (and the small-M rule): the first and last M of every 64-row
+    // range cover every image a call with M <= max_M picks
+    const int ranges = (std::max(max_M, 1) + tsg::kJit64TileM - 1) / tsg::kJit64TileM;
+    for (int r = 1; r <= ranges; r++) {
+        for (const int m : {(r - 1) * tsg::kJit64TileM + 1, std::min(std::max(max_M, 1), r * tsg::kJit64TileM)}) {
+            if (pick_ell_variant(h, m) >= 0) continue;  // the small-M kernel (its images below)
+            const bool r64 = pick_rows64(h, m);
+            const JitShape sh = pick_jit_shape(h, m, r64);
+            rc = ensure_jit_variant(h, sh.nw, sh.waves, nullptr, sh.far, r64);
+            if (rc) return rc;
+        }
     }
     // the small-M images calls with M <= max_M run: the choice only changes
     // at M = 1..4 (1-row tiles by M * N), past an M tile or past kEllMidM, so
@@ -1148,13 +1184,30 @@ extern "C" int tcsc_hip_set_jit_width(tsg_tcsc *h, int width)
 extern "C" int tcsc_hip_jit_width(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
-    return pick_jit_shape(h, M).nw;
+    return pick_jit_shape(h, M, pick_rows64(h, M)).nw;
 }
 
 extern "C" int tcsc_hip_jit_waves(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
-    return pick_jit_shape(h, M).waves;
+    return pick_jit_shape(h, M, pick_rows64(h, M)).waves;
+}
+
+extern "C" int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows)
+{
+    if (!h) return fail(TSG_ERR_ARG, "null handle");
+    if (rows != 0 && rows != 64 && rows != 128) return fail(TSG_ERR_ARG, "tcsc_hip_set_tile_rows: expected 0 (auto), 64 or 128");
+    if (rows == 64 && (h->kind != tsg_tcsc::kJit || h->B))
+        return fail(TSG_ERR_ARG, "tcsc_hip_set_tile_rows: the 64-row image computes plain TCSC on the jit kernel only");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->tile_rows = rows;
+    return TSG_OK;
+}
+
+extern "C" int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M)
+{
+    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
+    return pick_rows64(h, M) ? tsg::kJit64TileM : tsg::kJitTileM;
 }
 
 // Opt-in page-locking of a caller's host buffer (X or Y of repeated
@@ -1204,7 +1257,7 @@ extern "C" int tcsc_hip_set_far(tsg_tcsc *h, int mode)
 
 extern "C" int tcsc_hip_call_far(const tsg_tcsc *h, int M)
 {
-    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
+    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0 || pick_rows64(h, M)) return 0;
     return pick_jit_shape(h, M).far ? 1 : 0;
 }
 
@@ -1223,8 +1276,8 @@ extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)
 
 // The automatic per-call plan of a plain-TCSC handle with K, N and nnz
 // nonzeros at density split evenly (host only, no GPU: the same functions
-// run_dev uses on a handle).  kernel: 0 weight-compiled, 1 ELL walk, 2 ELL
-// producer/consumer walk.
+// run_dev uses on a handle).  kernel: 0 weight-compiled (128-row image), 1
+// ELL walk, 2 ELL producer/consumer walk, 3 weight-compiled 64-row image.
 extern "C" int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int *width, int *waves, int *far,
                              int *gn, int *gm, int *tmask)
 {
@@ -1240,16 +1293,17 @@ extern "C" int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int 
     h.nnz_neg = nnz / 2;
     h.jit_nch = std::max(1, (K + tsg::kJitChunk - 1) / tsg::kJitChunk);
     const int ev = pick_ell_variant(&h, M);
-    *kernel = ev < 0 ? 0 : use_ell_pc(&h, ev) ? 2 : 1;
+    const bool r64 = ev < 0 && pick_rows64(&h, M);
+    *kernel = ev >= 0 ? (use_ell_pc(&h, ev) ? 2 : 1) : r64 ? 3 : 0;
     *width = *waves = *far = *gn = *gm = *tmask = 0;
     if (ev < 0) {
-        const JitShape sh = pick_jit_shape(&h, M);
-        const int Mp = (M + tsg::kJitTileM - 1) / tsg::kJitTileM * tsg::kJitTileM;
+        const JitShape sh = pick_jit_shape(&h, M, r64);
+        const int tm = r64 ? tsg::kJit64TileM : tsg::kJitTileM;
         const int ntiles = (N + sh.nw * sh.waves - 1) / (sh.nw * sh.waves);
         *width = sh.nw;
         *waves = sh.waves;
         *far = sh.far ? 1 : 0;
-        pick_jit_map(&h, Mp / tsg::kJitTileM, ntiles, *gn, *gm, *tmask);
+        pick_jit_map(&h, (M + tm - 1) / tm, ntiles, *gn, *gm, *tmask);
     }
     return TSG_OK;
 }
@@ -1259,6 +1313,7 @@ extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)
     if (!h) return "";
     const int ev = pick_ell_variant(h, M);
     if (ev >= 0) return use_ell_pc(h, ev) ? "tsg_tcsc_ell_pc_kernel" : "tsg_tcsc_ell_kernel";
+    if (h->kind == tsg_tcsc::kJit && pick_rows64(h, M)) return "tsg_jit64_kernel";
     return h->kind == tsg_tcsc::kJit ? "tsg_jit_kernel" : "tsg_tcsc_rx_kernel";
 }
 
@@ -1269,8 +1324,8 @@ extern "C" int64_t tcsc_hip_call_image_bytes(tsg_tcsc *h, int M)
     const int ev = pick_ell_variant(h, M);
     if (ev >= 0) return h->ell[ev].ready ? h->ell[ev].bytes : 0;
     if (h->kind != tsg_tcsc::kJit) return (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
-    const JitShape sh = pick_jit_shape(h, M);
-    const tsg_tcsc::JitVariant &v = h->jv[shape_index(sh)];
+    const bool r64 = pick_rows64(h, M);
+    const tsg_tcsc::JitVariant &v = variant_of(h, pick_jit_shape(h, M, r64));
     return v.mod.function ? v.code_bytes + v.wcode_words * 4 : 0;
 }
 
@@ -1313,6 +1368,7 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     const bool jit = h->kind == tsg_tcsc::kJit;
     int64_t jit_bytes = 0;
     for (const auto &v : h->jv) jit_bytes += v.code_bytes + v.wcode_words * 4;
+    for (const auto &v : h->jv64) jit_bytes += v.code_bytes + v.wcode_words * 4;
     for (const auto &e : h->ell) jit_bytes += e.bytes;
     o->image_bytes = jit ? jit_bytes : (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;

@@ -98,6 +98,23 @@ constexpr uint32_t kJitM0kFlag = 1u << 16;
 // staged with non-temporal loads (tsg_capi.cpp far_xt)
 constexpr uint32_t kJitFarFlag = 1u << 17;
 
+// The 64-row image (round 4): one M row per lane, 64-row M
+// tiles, every nonzero one 4-byte VOP2 `v_add_f32 acc, acc, x` (+1) or
+// `v_sub_f32 acc, acc, x` (-1) on one accumulator VGPR per column -- half the
+// code bytes per useful add of the 128-row image when M <= 64 (whose
+// v_pk_add_f32 then works on 64 padding rows).  X^T in the k-quad layout
+// (tsg_transpose_quads_kernel): for k-row quad q and M row m the 16 bytes at
+// (q * Mp + m) * 16 hold X[m][4q .. 4q+3], so one ds_read_b128 of lane l
+// (row m0 + l) loads four k rows of its row into an X slot (rows 4q+j in
+// v[s+j]; ds_read_b64 / b32 for quads with 2 / 1 used rows).  An M tile's
+// slice of a quad row is 64 lanes x 16 B = 1 KiB: one LDS-DMA piece, as in
+// the k-pair layout, so the ring, the DMA pieces and the register contract
+// are the 128-row image's; chunks are 192 K rows (48 quads, 48 KiB).
+// Dispatchers lib/tsg_jit64_w<nw>[_4w].co (kernel tsg_jit64_kernel).
+constexpr int kJit64TileM = 64;
+constexpr int kJit64Chunk = 192;
+constexpr uint32_t kJit64Format = 3;                    // region header word 7 bits 8-15: k-quad layout
+
 // Stream width: columns per generated stream.  kJitNW (64) is the default;
 // narrower streams (32, 16, 8: same register contract, fewer accumulators,
 // dispatcher lib/tsg_jit_w<nw>.co) give small-M calls more workgroups
@@ -114,26 +131,29 @@ constexpr int kJitTailPadWords = 32768 + 1024;
 
 struct JitImage {
     int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0, waves = kJitWaves;
+    int tile_m = kJitTileM, chunk = kJitChunk;  // 64 / kJit64Chunk for the 64-row image
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
     std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
 };
 // B = 0: BaseTCSC order (comp.h:25-69); B > 0: BaseBlockedTCSC<B> order
 // (comp.h:607-658) from BlockedTCSC<B> arrays
+// rows64: the 64-row image (plain TCSC only; BaseTCSC order, VOP2 adds)
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                     const int32_t *rin, int K, int N, int B, JitImage &img, int nw = kJitNW,
-                    int waves = kJitWaves, bool far = false);
+                    int waves = kJitWaves, bool far = false, bool rows64 = false);
 
 struct JitModule {
     void *module = nullptr;        // hipModule_t
     void *function = nullptr;      // hipFunction_t of tsg_jit_kernel
     void *probe = nullptr;         // hipFunction_t of tsg_jit_probe (region check, at load)
-    std::string load(const std::vector<uint32_t> &code, int nw = kJitNW, int waves = kJitWaves);  // "" on success
+    std::string load(const std::vector<uint32_t> &code, int nw = kJitNW, int waves = kJitWaves,
+                     bool rows64 = false);  // "" on success
     void unload();
 };
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                     int prelu, uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask,
-                    void *stream);
+                    void *stream, int tile_m = kJitTileM);
 int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream);
 
 // ---------------------------------------------------------------------------
@@ -192,6 +212,8 @@ int encode_fill(const int32_t *dW, int K, int N, const int32_t *d_csp, const int
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream);
 // X [M][K] -> X^T in the k-pair layout of the jit kernel (Kp even, Mp even)
 int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int Kp, void *stream);
+// X [M][K] -> X^T in the k-quad layout of the 64-row image (Mp % 64 == 0, Kp % 64 == 0)
+int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, void *stream);
 int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                    const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                    int prelu, void *stream);

@@ -63,6 +63,20 @@ struct Emit {
         c.push_back(0xd3b24000u | d);
         c.push_back((3u << 27) | ((256u + t) << 9) | (256u + d));
     }
+    // 64-row image: v_add_f32 v[d], v[d], v[x] / v_sub_f32 v[d], v[d], v[x]
+    // (VOP2, 4 bytes: d = d + x for a +1 entry, d = d - x for a -1 entry --
+    // comp.h:47 `y += x` and comp.h:57 `y -= x` on one M row per lane)
+    void v_addsub(uint32_t d, uint32_t x, bool neg)
+    {
+        c.push_back(((neg ? 2u : 1u) << 25) | (d << 17) | (x << 9) | (256u + d));
+    }
+    // ds_read_b32 v[d], v[a] offset:off
+    void ds_read_b32(uint32_t d, uint32_t a, uint32_t off)
+    {
+        align8();
+        c.push_back(0xd86c0000u | off);
+        c.push_back((d << 24) | a);
+    }
     // ds_read_b64 v[d:d+1], v[a] offset:off
     void ds_read_b64(uint32_t d, uint32_t a, uint32_t off)
     {
@@ -123,9 +137,11 @@ struct Emit {
 // VGPRs: one k-row pair each), then kJitRing LDS buffer bases (buffer + lane *
 // 16), the code-prefetch sink, the DMA piece offsets, lane*128, and the
 // accumulators from the next even register.
-constexpr uint32_t kPairBytes = kJitTileM * 8;            // one k-row pair of the tile in LDS: 1 KiB
+constexpr uint32_t kPairBytes = kJitTileM * 8;            // one k-row pair (64-row image: quad) of the tile in LDS: 1 KiB
 constexpr uint32_t kBufBytes = kJitChunk / 2 * kPairBytes; // one LDS chunk buffer (48 KiB)
 static_assert(kPairBytes == 1024, "one LDS-DMA piece (64 lanes x 16 B) is one pair row");
+static_assert(kJit64TileM * 16 == (int)kPairBytes && kJit64Chunk / 4 == kJitChunk / 2,
+              "64-row image: a quad row is one 1-KiB piece, 48 of them per chunk (the same ring)");
 constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 4s : 11 + 4s]
 constexpr uint32_t kLdsBaseV = kXSlot0 + kJitXRegs;        // + b: buffer b + lane * 16
 constexpr uint32_t kSinkV = kLdsBaseV + kJitRing;
@@ -148,17 +164,35 @@ static_assert(((kDmaOffV + kJitChunk / 2 / 4 + 2) & ~1u) + 2 * 32 <= 256u, "VGPR
 constexpr int kTailPad = kJitTailPadWords;  // words of padding after the last stream (code prefetch reads ahead)
 static_assert((kJitChunk / 2 - 1) * kPairBytes + 8 < 65536, "ds_read offset field");
 
-// One step's work for a wave: its X reads (k-row pairs of the chunk with an
-// entry in the step, ascending) and, per read, the columns with an entry in
-// the even / odd row of the pair.
+// One step's work for a wave: its X reads (k-row units of the chunk with an
+// entry in the step, ascending: pairs, or quads in the 64-row image) and, per
+// read, the columns with an entry in each row of the unit.
 struct Section {
     struct Read {
-        int pair = 0;
-        int mask = 0;                      // 1: even row used, 2: odd row, 3: both
-        std::vector<uint8_t> cols[2];
+        int pair = 0;                      // unit index in the chunk (pair / quad)
+        int mask = 0;                      // bit r: row r of the unit used
+        std::vector<uint8_t> cols[4];
     };
     std::vector<Read> reads;
 };
+
+// 64-row image: how a quad with used-row mask `mask` is read -- byte offset in
+// the quad, VGPRs loaded and the first row they hold (ds_read_b32 / b64 for
+// quads with one used row / rows only in one half, else ds_read_b128)
+struct QuadRead {
+    uint32_t off;
+    int nreg, row0;
+};
+QuadRead quad_read(int mask)
+{
+    if (mask == 1 || mask == 2 || mask == 4 || mask == 8) {
+        const int r = mask == 1 ? 0 : mask == 2 ? 1 : mask == 4 ? 2 : 3;
+        return {(uint32_t)r * 4u, 1, r};
+    }
+    if ((mask & ~3) == 0) return {0u, 2, 0};
+    if ((mask & 3) == 0) return {8u, 2, 2};
+    return {0u, 4, 0};
+}
 
 // One step of a stream: the X^T chunk staged into LDS buffer q % kJitRing and which
 // of its entries the step adds.
@@ -179,10 +213,9 @@ struct StepSpec {
 // a wave runs its columns in two halves (y of half the columns in the upper
 // X-slot registers); per half, block by block: pass 0 over the chunks the
 // block touches, pass 1, then Y += y.
-std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw)
+std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw, int C = kJitChunk)
 {
     std::vector<StepSpec> plan;
-    const int C = kJitChunk;
     if (!B) {
         for (int p = 0; p < 2; p++)
             for (int j = 0; j < nch; j++) plan.push_back({j, p, 0, nw, j * C, j * C + C, 0, j == 0, false});
@@ -203,10 +236,15 @@ std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw)
 }  // namespace
 
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
-                    int K, int N, int B, JitImage &img, int nw, int waves, bool far)
+                    int K, int N, int B, JitImage &img, int nw, int waves, bool far, bool r64)
 {
     if (nw <= 0) nw = kJitNW;
     if (!jit_waves_ok(nw, waves)) waves = kJitWaves;
+    if (B) r64 = false;  // BlockedTCSC: the 128-row image only
+    if (r64) far = false;
+    // K rows per chunk and per LDS unit (a pair, or a quad in the 64-row image):
+    // 48 units of 1 KiB per chunk either way
+    const int CH = r64 ? kJit64Chunk : kJitChunk, U = r64 ? 4 : 2;
     const JitRegs R(waves);
     const int streams = waves;  // one stream per wave (no M split)
     const int kPieces = R.pieces;
@@ -217,10 +255,12 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     img.B = B;
     img.nw = nw;
     img.waves = waves;
+    img.tile_m = r64 ? kJit64TileM : kJitTileM;
+    img.chunk = CH;
     img.Npad = ((N + tile_cols - 1) / tile_cols) * tile_cols;
-    img.nch = std::max(1, (K + kJitChunk - 1) / kJitChunk);
+    img.nch = std::max(1, (K + CH - 1) / CH);
     const int nch = img.nch, ntiles = img.Npad / tile_cols;
-    const std::vector<StepSpec> plan = plan_steps(K, N, B, nch, nw);
+    const std::vector<StepSpec> plan = plan_steps(K, N, B, nch, nw, CH);
     const int steps = (int)plan.size();
     // LDS-DMA issue (TSG_JIT_DMA="spread,m0k" overrides, A/B): the pieces that
     // stage step q + kJitRing - 1 go out spread over the first `spread` of step
@@ -268,11 +308,11 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // register contract from it), the block size, the X slots in use, the
     // ring and the X^T layout
     code.insert(code.end(), {kJitMagic0, kJitMagic1,
-                             (uint32_t)waves | (uint32_t)nw << 8 | (uint32_t)kJitChunk << 16,
-                             (uint32_t)kJitSlots | (uint32_t)kJitTileM << 16,
+                             (uint32_t)waves | (uint32_t)nw << 8 | (uint32_t)CH << 16,
+                             (uint32_t)kJitSlots | (uint32_t)img.tile_m << 16,
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
-                             (uint32_t)kJitRing | kJitFormat << 8 | (uint32_t)(m0k ? kJitM0kFlag : 0u) |
-                                 (far ? kJitFarFlag : 0u)});
+                             (uint32_t)kJitRing | (r64 ? kJit64Format : kJitFormat) << 8 |
+                                 (uint32_t)(m0k ? kJitM0kFlag : 0u) | (far ? kJitFarFlag : 0u)});
     const char *na = knob_value("TSG_JIT_NOALIGN");
     Emit E{code, !(na && na[0] == '1')};
     // TSG_JIT_CP="dma,touch": cache-policy bits of the LDS-DMA pieces and the
@@ -317,7 +357,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // per row the columns with an entry there
     auto build_section = [&](int q, Section &sec) {
         const StepSpec &sp = plan[(size_t)q];
-        const int p = sp.pass, kc = sp.chunk * kJitChunk;
+        const int p = sp.pass, kc = sp.chunk * CH;
         const int32_t *cs = p ? csn : csp, *ri = p ? rin : rip;
         if (sp.reset)
             for (int col = sp.c0; col < sp.c1; col++) {
@@ -325,22 +365,22 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 cur[(size_t)col * 2 + p] = n < N ? cs[sp.slot0 + n] : 0;
                 end[(size_t)col * 2 + p] = n < N ? cs[sp.slot0 + n + 1] : 0;
             }
-        std::vector<std::vector<uint8_t>> by_row(kJitChunk);
+        std::vector<std::vector<uint8_t>> by_row(CH);
         for (int col = sp.c0; col < sp.c1; col++) {
             int32_t &i = cur[(size_t)col * 2 + p];
             const int32_t e = end[(size_t)col * 2 + p];
             for (; i < e && ri[i] < sp.khi; i++) by_row[ri[i] - kc].push_back((uint8_t)col);
         }
         sec.reads.clear();
-        for (int pr = 0; pr < kJitChunk / 2; pr++) {
-            const bool lo = !by_row[2 * pr].empty(), hi = !by_row[2 * pr + 1].empty();
-            if (!lo && !hi) continue;
+        for (int pr = 0; pr < CH / U; pr++) {
             Section::Read rd;
             rd.pair = pr;
-            rd.mask = (lo ? 1 : 0) | (hi ? 2 : 0);
-            if (lo) rd.cols[0] = std::move(by_row[2 * pr]);
-            if (hi) rd.cols[1] = std::move(by_row[2 * pr + 1]);
-            sec.reads.push_back(std::move(rd));
+            for (int r = 0; r < U; r++)
+                if (!by_row[U * pr + r].empty()) {
+                    rd.mask |= 1 << r;
+                    rd.cols[r] = std::move(by_row[U * pr + r]);
+                }
+            if (rd.mask) sec.reads.push_back(std::move(rd));
         }
     };
     int base_chunk = -1;  // chunk whose base s[84:85] holds
@@ -392,9 +432,12 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         G = std::max(1, S / 3);
         RA = S - G;
     }
-    // register of row `half` (0: even k, 1: odd k) of read g
+    // register of row `half` of read g's unit (pair: 0 even k, 1 odd k, two
+    // VGPRs each; quad: row r of the four, one VGPR each)
     auto xreg = [&](int64_t g, const Section::Read &rd, int half) {
-        return kXSlot0 + (uint32_t)(kJitSlotRegs * (g % S)) + (rd.mask == 3 ? 2u * (uint32_t)half : 0u);
+        const uint32_t slot = kXSlot0 + (uint32_t)(kJitSlotRegs * (g % S));
+        if (r64) return slot + (uint32_t)(half - quad_read(rd.mask).row0);
+        return slot + (rd.mask == 3 ? 2u * (uint32_t)half : 0u);
     };
     for (int t = 0; t < ntiles; t++) {
         for (int w = 0; w < streams; w++) {
@@ -432,8 +475,16 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     if (d_noreads) continue;
                     const uint32_t dst = kXSlot0 + (uint32_t)(kJitSlotRegs * (issued % S));
                     const uint32_t lb = kLdsBaseV + (uint32_t)(rq % kJitRing), off = (uint32_t)rd.pair * kPairBytes;
-                    if (rd.mask == 3) E.ds_read_b128(dst, lb, off);
-                    else E.ds_read_b64(dst, lb, off + (rd.mask == 2 ? 8u : 0u));
+                    if (r64) {
+                        const QuadRead qr = quad_read(rd.mask);
+                        if (qr.nreg == 4) E.ds_read_b128(dst, lb, off);
+                        else if (qr.nreg == 2) E.ds_read_b64(dst, lb, off + qr.off);
+                        else E.ds_read_b32(dst, lb, off + qr.off);
+                    } else if (rd.mask == 3) {
+                        E.ds_read_b128(dst, lb, off);
+                    } else {
+                        E.ds_read_b64(dst, lb, off + (rd.mask == 2 ? 8u : 0u));
+                    }
                 }
             };
             auto wait_reads = [&](int64_t upto) {  // reads < upto complete
@@ -449,6 +500,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 // one entry: BaseTCSC adds into the column's accumulator; a
                 // BlockedTCSC block chains in y (0 + first entry, then in place)
                 auto add = [&](int col, uint32_t x) {
+                    if (r64) {  // one accumulator VGPR per column
+                        E.v_addsub(kAcc0 + (uint32_t)col, x, neg);
+                        return;
+                    }
                     if (!B) {
                         E.pk_add(kAcc0 + 2u * (uint32_t)col, x, neg);
                         return;
@@ -504,7 +559,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     std::vector<std::vector<uint32_t>> xs(nw);
                     for (int i = i0; i < i1; i++) {
                         const Section::Read &rd = sec.reads[(size_t)i];
-                        for (int half = 0; half < 2; half++)
+                        for (int half = 0; half < U; half++)
                             for (uint8_t col : rd.cols[half]) xs[col].push_back(xreg(first[q] + i, rd, half));
                     }
                     for (int col = sp.c0; col < sp.c1; col += 2)
@@ -543,10 +598,12 @@ namespace {
 
 // The dispatcher of a stream width: lib/tsg_jit.co (kJitNW columns per wave)
 // or lib/tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile);
-// 4-wave workgroups: lib/tsg_jit_w<nw>_4w.co (TSG_JIT_WAVES=4).
-std::string template_path(int nw, int waves)
+// 4-wave workgroups: lib/tsg_jit_w<nw>_4w.co (TSG_JIT_WAVES=4); the 64-row
+// image: lib/tsg_jit64_w<nw>[_4w].co (TSG_JIT_ROWS64=1).
+std::string template_path(int nw, int waves, bool r64)
 {
-    const std::string name = nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
+    const std::string name = r64 ? "tsg_jit64_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co"
+                             : nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
                              : "tsg_jit_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co";
     if (const char *dir = knob_value("TSG_JIT_DIR")) return std::string(dir) + "/" + name;  // tests: rx fallback
     Dl_info info;
@@ -560,9 +617,9 @@ std::string template_path(int nw, int waves)
 
 }  // namespace
 
-std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves)
+std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves, bool r64)
 {
-    const std::string path = template_path(nw, waves);
+    const std::string path = template_path(nw, waves, r64);
     std::ifstream f(path, std::ios::binary);
     if (!f) return "cannot open jit template " + path;
     std::vector<unsigned char> img((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -622,7 +679,7 @@ std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves
     hipError_t e = hipModuleLoadData(&m, img.data());
     if (e != hipSuccess) return std::string("hipModuleLoadData: ") + hipGetErrorString(e);
     hipFunction_t fn = nullptr, pf = nullptr;
-    e = hipModuleGetFunction(&fn, m, "tsg_jit_kernel");
+    e = hipModuleGetFunction(&fn, m, r64 ? "tsg_jit64_kernel" : "tsg_jit_kernel");
     if (e == hipSuccess) e = hipModuleGetFunction(&pf, m, "tsg_jit_probe");
     if (e != hipSuccess) {
         (void)hipModuleUnload(m);
@@ -652,9 +709,10 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream)
 
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
-                    uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask, void *stream)
+                    uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask, void *stream,
+                    int tile_m)
 {
-    int mtiles = Mp / kJitTileM, ntiles = Npad / tile_cols;
+    int mtiles = Mp / tile_m, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
                       (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask};
@@ -702,6 +760,38 @@ extern "C" int tsg_jit_codegen_wv(const int32_t *csp, const int32_t *csn, const 
     if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
     if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
         g_tsg_host_err = "tsg_jit_codegen: buffer too small";
+        return TSG_ERR_ARG;
+    }
+    if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);
+    if (wcode) std::memcpy(wcode, img.wcode.data(), img.wcode.size() * 4);
+    return TSG_OK;
+}
+
+extern "C" int tsg_jit_codegen64(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                                 int K, int N, int width, int waves, uint32_t *code, int64_t code_cap,
+                                 int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
+{
+    if (!tsg::jit_width_ok(width) || !tsg::jit_waves_ok(width, waves)) {
+        g_tsg_host_err = "tsg_jit_codegen64: unsupported shape " + std::to_string(width) + " x " +
+                         std::to_string(waves) + " (widths 64, 32, 16, 8; 4 waves for the narrow ones)";
+        return TSG_ERR_ARG;
+    }
+    const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, 0);
+    if (!e.empty()) {
+        g_tsg_host_err = "tsg_jit_codegen64: malformed TCSC: " + e;
+        return TSG_ERR_ARG;
+    }
+    const std::string ke = tsg::knob_check();
+    if (!ke.empty()) {
+        g_tsg_host_err = "tsg_jit_codegen64: " + ke;
+        return TSG_ERR_ARG;
+    }
+    tsg::JitImage img;
+    tsg::build_jit_code(csp, csn, rip, rin, K, N, 0, img, width, waves, false, true);
+    if (code_len) *code_len = (int64_t)img.code.size();
+    if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
+    if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
+        g_tsg_host_err = "tsg_jit_codegen64: buffer too small";
         return TSG_ERR_ARG;
     }
     if (code) std::memcpy(code, img.code.data(), img.code.size() * 4);

@@ -57,21 +57,39 @@ namespace {
 #ifndef TSG_JIT_WAVES
 #define TSG_JIT_WAVES 8
 #endif
+// TSG_JIT_ROWS64=1: the 64-row image's dispatcher (lib/tsg_jit64_w<NW>[_4w].co,
+// kernel tsg_jit64_kernel; tsg_internal.h): one M row per lane, 64-row M
+// tiles, one accumulator VGPR per column, X^T in the k-quad layout, 192-row
+// chunks (48 quads) -- the same ring, DMA pieces and register contract
+#ifndef TSG_JIT_ROWS64
+#define TSG_JIT_ROWS64 0
+#endif
 constexpr int kJWaves = TSG_JIT_WAVES;
 constexpr int kJNW = TSG_JIT_NW;
 static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8, "stream width");
 static_assert(kJWaves == 8 || (kJWaves == 4 && kJNW < 64), "waves per workgroup");
-constexpr int kJTileM = 128;
+constexpr bool kJRows64 = TSG_JIT_ROWS64 != 0;
+constexpr int kJTileM = kJRows64 ? 64 : 128;
+constexpr int kJRowsPerLane = kJTileM / 64;
 constexpr int kJTileCols = kJWaves * kJNW;
 constexpr int kJRing = 3;                            // LDS buffers in the X^T ring (tsg_internal.h)
-constexpr int kJChunk = 96;                          // K rows per chunk = 48 k-row pairs
+constexpr int kJChunk = kJRows64 ? 192 : 96;         // K rows per chunk = 48 k-row quads / pairs
+constexpr int kJUnits = kJRows64 ? kJChunk / 4 : kJChunk / 2;  // 1-KiB LDS units per chunk
 constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB
-constexpr int kJPieces = kJChunk / 2 / kJWaves;      // LDS-DMA pieces (1-KiB pair rows) per wave per chunk
+constexpr int kJPieces = kJUnits / kJWaves;          // LDS-DMA pieces (1-KiB unit rows) per wave per chunk
+static_assert(kJBufBytes == kJUnits * 1024, "one LDS-DMA piece per unit row");
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
 constexpr uint32_t kJM0kFlag = 1u << 16;  // header word 7: piece offsets in the DMA instruction (tsg_internal.h)
+constexpr uint32_t kJFormat = kJRows64 ? 3u : 2u;  // header word 7 bits 8-15: the X^T layout the code expects
+#if TSG_JIT_ROWS64
+#define TSG_JIT_KERNEL_NAME tsg_jit64_kernel
+#else
+#define TSG_JIT_KERNEL_NAME tsg_jit_kernel
+#endif
 
 typedef float F32x32 __attribute__((ext_vector_type(32)));
 typedef float F32x16 __attribute__((ext_vector_type(16)));
+typedef float F32x8 __attribute__((ext_vector_type(8)));
 
 #if TSG_JIT_WAVES == 8
 #define TSG_JIT_IN                                                                                  \
@@ -120,7 +138,7 @@ extern "C" __global__ __launch_bounds__(64) void tsg_jit_probe(uint32_t *__restr
     }
 }
 
-extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
+extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
@@ -142,9 +160,9 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  : "={s[92:93]}"(base)
                  :
                  : "scc");
-    // never jump into a region that is not ours
+    // never jump into a region that is not ours (or laid out for the other image)
     const uint32_t *hdr = reinterpret_cast<const uint32_t *>(base);
-    if (hdr[0] != kJMagic0 || hdr[1] != kJMagic1) {
+    if (hdr[0] != kJMagic0 || hdr[1] != kJMagic1 || ((hdr[7] >> 8) & 0xffu) != kJFormat) {
         if (blockIdx.x == 0 && tid == 0) status[0] = 1u;
         return;
     }
@@ -159,7 +177,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
     const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + stream]);
     const uint32_t lb0 = (uint32_t)lane * 16u, lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
     // LDS-DMA piece i of this wave = pair row pr = wave * P + i of the chunk: the
-    // lane's 16 B at ((pr * Mp/2) + m0/2 + lane) * 16 from the chunk base.  With
+    // lane's 16 B at ((pr * Mp/2) + m0/2 + lane) * 16 from the chunk base (64-row
+    // image: quad row pr, ((pr * Mp) + m0 + lane) * 16).  With
     // the header's m0k flag the generated code adds (i & 3) KiB through the
     // instruction offset (to the LDS and the global address alike): subtracted
     // here (never negative: pr >= i and a pair row of X^T is >= 1 KiB)
@@ -168,7 +187,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
 #pragma unroll
     for (int i = 0; i < kJPieces; i++) {
         const uint32_t pr = (uint32_t)(wave * kJPieces + i);
-        off[i] = (pr * ((uint32_t)Mp / 2u) + (uint32_t)m0 / 2u + (uint32_t)lane) * 16u - m0k * (uint32_t)(i & 3) * 1024u;
+        off[i] = (pr * ((uint32_t)Mp / kJRowsPerLane) + (uint32_t)m0 / kJRowsPerLane + (uint32_t)lane) * 16u -
+                 m0k * (uint32_t)(i & 3) * 1024u;
     }
     const uint32_t wb = (uint32_t)(wave * kJPieces) * 1024u;  // s83
     // code touch (one dword per 128-B line of the stream ahead, into L2): only
@@ -189,7 +209,35 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb), \
                    TSG_JIT_IN                                                                       \
                  : TSG_JIT_CLOBBERS)
-#if TSG_JIT_WAVES == 8 && TSG_JIT_NW == 64
+#if TSG_JIT_ROWS64  // one accumulator VGPR per column (acc0 = v116; 4 waves: v122)
+#if TSG_JIT_WAVES == 8
+#define TSG_JIT_A0 "v[116:147]"
+#define TSG_JIT_A1 "v[148:179]"
+#define TSG_JIT_A16 "v[116:131]"
+#define TSG_JIT_A8 "v[116:123]"
+#else
+#define TSG_JIT_A0 "v[122:153]"
+#define TSG_JIT_A16 "v[122:137]"
+#define TSG_JIT_A8 "v[122:129]"
+#endif
+#if TSG_JIT_NW == 64
+    F32x32 a0 = {}, a1 = {};  // comp.h:41
+    TSG_JIT_CALL("+{" TSG_JIT_A0 "}"(a0), "+{" TSG_JIT_A1 "}"(a1));
+    auto acc_of = [&](int c, int) { return c < 32 ? a0[c] : a1[c - 32]; };
+#elif TSG_JIT_NW == 32
+    F32x32 a0 = {};  // comp.h:41
+    TSG_JIT_CALL("+{" TSG_JIT_A0 "}"(a0));
+    auto acc_of = [&](int c, int) { return a0[c]; };
+#elif TSG_JIT_NW == 16
+    F32x16 a0 = {};  // comp.h:41
+    TSG_JIT_CALL("+{" TSG_JIT_A16 "}"(a0));
+    auto acc_of = [&](int c, int) { return a0[c]; };
+#else
+    F32x8 a0 = {};  // comp.h:41
+    TSG_JIT_CALL("+{" TSG_JIT_A8 "}"(a0));
+    auto acc_of = [&](int c, int) { return a0[c]; };
+#endif
+#elif TSG_JIT_WAVES == 8 && TSG_JIT_NW == 64
     F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
     TSG_JIT_CALL("+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3));
     auto acc_of = [&](int c, int r) {
@@ -225,8 +273,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void tsg_jit_kernel(
 
     if (ncol0 >= N) return;
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const int m = m0 + 2 * lane + r;
+    for (int r = 0; r < kJRowsPerLane; r++) {
+        const int m = m0 + kJRowsPerLane * lane + r;
         if (m >= M) continue;
         float *yrow = Y + (size_t)m * N + ncol0;
         float v[kJNW];

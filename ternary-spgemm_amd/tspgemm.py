@@ -46,7 +46,8 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
     "tcsc_hip_host_register", "tcsc_hip_host_unregister", "tcsc_hip_set_far", "tcsc_hip_call_far",
-    "tsg_jit_codegen_far", "tsg_call_plan", "tsg_knob_check",
+    "tsg_jit_codegen_far", "tsg_call_plan", "tsg_knob_check", "tcsc_hip_set_tile_rows", "tcsc_hip_call_tile_rows",
+    "tsg_jit_codegen64",
 )
 
 
@@ -130,6 +131,10 @@ def lib() -> C.CDLL:
                                      C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tcsc_hip_set_small_m.argtypes = [H, C.c_int]
     L.tcsc_hip_set_far.argtypes = [H, C.c_int]
+    L.tcsc_hip_set_tile_rows.argtypes = [H, C.c_int]
+    L.tcsc_hip_call_tile_rows.argtypes = [H, C.c_int]
+    L.tsg_jit_codegen64.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
+                                    C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tsg_call_plan.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int] + [C.POINTER(C.c_int)] * 7
     L.tcsc_hip_call_far.argtypes = [H, C.c_int]
     L.tsg_jit_codegen_far.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
@@ -271,6 +276,21 @@ def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0, width: int = 64,
     return code, wcode
 
 
+def jit_codegen64(csp, csn, rip, rin, K: int, N: int, width: int = 16, waves: int = 4):
+    """Host-side machine code of the 64-row image (one M row per lane, VOP2
+    adds, k-quad X^T; include/ternary_spgemm_test.h tsg_jit_codegen64)."""
+    csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
+    nc, nw = C.c_int64(), C.c_int64()
+    L = lib()
+    _check(L.tsg_jit_codegen64(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, width, waves, None, 0, C.byref(nc),
+                               None, 0, C.byref(nw)), "tsg_jit_codegen64")
+    code = np.empty(nc.value, np.uint32)
+    wcode = np.empty(nw.value, np.uint32)
+    _check(L.tsg_jit_codegen64(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, width, waves, _ptr(code), nc.value,
+                               C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)), "tsg_jit_codegen64")
+    return code, wcode
+
+
 def jit_codegen_far(csp, csn, rip, rin, K: int, N: int):
     """The far-X^T image of the 64-wide plain-TCSC code (no code touches,
     non-temporal X^T staging; include/ternary_spgemm.h tcsc_hip_set_far)."""
@@ -293,7 +313,7 @@ def call_plan(K: int, N: int, nnz: int, M: int) -> dict:
     v = [C.c_int() for _ in range(7)]
     _check(lib().tsg_call_plan(K, N, nnz, M, *[C.byref(x) for x in v]), "tsg_call_plan")
     kernel, width, waves, far, gn, gm, tmask = (x.value for x in v)
-    return {"kernel": ("tsg_jit_kernel", "tsg_tcsc_ell_kernel", "tsg_tcsc_ell_pc_kernel")[kernel],
+    return {"kernel": ("tsg_jit_kernel", "tsg_tcsc_ell_kernel", "tsg_tcsc_ell_pc_kernel", "tsg_jit64_kernel")[kernel],
             "width": width, "waves": waves, "far": bool(far), "map": (gn, gm), "tmask": tmask}
 
 
@@ -624,6 +644,16 @@ class TCSCDevice:
         """Far-X^T code image: 0 = automatic (default), 1 = never, 2 = every
         64-wide call."""
         _check(lib().tcsc_hip_set_far(self._h, mode), "tcsc_hip_set_far")
+
+    def set_tile_rows(self, rows: int) -> None:
+        """Weight-compiled image: 0 = automatic (default), 64 = the 64-row
+        image (one row per lane, VOP2 adds), 128 = the 128-row image."""
+        _check(lib().tcsc_hip_set_tile_rows(self._h, rows), "tcsc_hip_set_tile_rows")
+
+    def call_tile_rows(self, M: int) -> int:
+        """M tile (64 / 128) of the weight-compiled image a call with M rows
+        runs; 0 when it runs a small-M walk."""
+        return int(lib().tcsc_hip_call_tile_rows(self._h, M))
 
     def call_far(self, M: int) -> bool:
         """True if a call with M rows runs the far-X^T image."""

@@ -31,16 +31,22 @@ class Geom:
         self.waves, self.nw, self.chunk = w2 & 0xFF, (w2 >> 8) & 0xFF, w2 >> 16
         self.slots, self.tile_m = w3 & 0xFFFF, w3 >> 16
         self.streams, self.msplit = w4 & 0xFF, (w4 >> 8) & 0xFF
-        assert self.streams == self.waves and self.msplit == 1 and self.tile_m == 128
         self.tile_cols = self.streams * self.nw
         self.ring = int(code[7]) & 0xFF
-        assert (int(code[7]) >> 8) & 0xFF == 2, "region must use the k-pair X^T layout (format 2)"
+        fmt = (int(code[7]) >> 8) & 0xFF
+        # format 2: k-pair X^T, 128-row tiles, v_pk_add_f32 (2 rows per lane);
+        # format 3: the 64-row image -- k-quad X^T, 64-row tiles, VOP2 adds
+        assert fmt in (2, 3), "region must use the k-pair (2) or k-quad (3) X^T layout"
+        self.r64 = fmt == 3
+        assert self.streams == self.waves and self.msplit == 1 and self.tile_m == (64 if self.r64 else 128)
         # DMA pieces take their in-group offset from the instruction offset (one
         # M0 per 4 pieces; the dispatcher subtracts it from the global offsets)
         self.m0k = (int(code[7]) >> 16) & 1
         assert int(code[7]) >> 18 == 0  # bit 16: m0k, bit 17: far-X^T image
-        self.pairs = self.chunk // 2                  # k-row pairs per chunk
-        self.pair_bytes = self.tile_m * 8             # one pair row of the tile in LDS: 1 KiB
+        self.unit = 4 if self.r64 else 2              # k rows per LDS unit (quad / pair)
+        self.pairs = self.chunk // self.unit          # units per chunk
+        self.pair_bytes = self.tile_m * 4 * self.unit  # one unit row of the tile in LDS: 1 KiB
+        assert self.pair_bytes == 1024
         self.buf_bytes = self.pairs * self.pair_bytes
         self.pieces = self.pairs // self.waves        # DMA pieces (pair rows) per wave
         self.lds_v = 8 + 4 * self.slots               # X slots: 4 VGPRs each
@@ -101,6 +107,11 @@ def _classify_pk(w0, w1, G):
 def _decode(code, pc, G):
     w0 = int(code[pc])
     w1 = int(code[pc + 1]) if pc + 1 < len(code) else None
+    if G.r64 and (w0 >> 31) == 0:  # VOP2: v_add_f32 (op 1) / v_sub_f32 (op 2) acc, acc, x
+        op, d, x, s0 = (w0 >> 25) & 0x3F, (w0 >> 17) & 0xFF, (w0 >> 9) & 0xFF, w0 & 0x1FF
+        assert op in (1, 2) and s0 == 256 + d, f"unexpected VOP2 word {w0:#010x}"
+        assert G.acc0 <= d < G.acc0 + G.nw and 8 <= x < 8 + 4 * G.xslots
+        return "vadd", (d, x, op == 2), 1
     if (w0 & 0xFFFFFFF0) == 0xBF800000:
         return "nop", (), 1
     if (w0 & 0xFFFFF0FF) == 0xBF8CC07F:
@@ -126,6 +137,9 @@ def _decode(code, pc, G):
     if (w0 & 0xFFFFFC00) == 0xD3B24000:  # v_pk_add_f32
         kind, f = _classify_pk(w0, w1, G)
         return kind, f, 2
+    if G.r64 and (w0 & 0xFFFF0000) == 0xD86C0000:  # ds_read_b32
+        assert (w1 >> 8) & 0xFFFF == 0
+        return "read", (w1 >> 24, w1 & 0xFF, w0 & 0xFFFF, 1), 2
     if (w0 & 0xFFFF0000) == 0xD8EC0000:  # ds_read_b64
         assert (w1 >> 8) & 0xFFFF == 0
         return "read", (w1 >> 24, w1 & 0xFF, w0 & 0xFFFF, 2), 2
@@ -153,8 +167,9 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
     last_read = np.full(NBUF * PAIRS, -1)
     S = G.streams
     waves = [Wave(w, int(wcode[t * S + w]) // 4) for w in range(WAVES)]
+    RPL = 1 if G.r64 else 2  # M rows per lane
     for wv in waves:
-        wv.v[G.acc0:G.acc0 + 2 * NW] = 0.0
+        wv.v[G.acc0:G.acc0 + RPL * NW] = 0.0
         assert int(wcode[t * S + wv.w]) % 256 == 0
     phase = 0
     while not all(wv.done for wv in waves):
@@ -198,7 +213,7 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     assert rem == 0 and 0 <= j < nch
                     dst = wv.m0 + off  # the offset applies to the LDS address too
                     assert dst % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
-                    data = XP[j * PAIRS + pr, m0 // 2:m0 // 2 + 64].reshape(-1).copy()
+                    data = XP[j * PAIRS + pr, m0 // RPL:m0 // RPL + 64].reshape(-1).copy()
                     wv.pending.append([(dst, data, phase)])
                 elif kind == "wait_vm":  # loads return in order: all but the newest f[0] land
                     n_land = max(len(wv.pending) - f[0], 0)
@@ -218,13 +233,18 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     wv.reads.append((vd, nreg))
                     assert G.lds_v <= a < G.lds_v + NBUF and off // PAIR_BYTES < PAIRS
                     assert 8 <= vd and vd + nreg <= 8 + 4 * G.xslots and (vd - 8) % 4 == 0
-                    half = (off % PAIR_BYTES) // 8
-                    assert off % 8 == 0 and off % PAIR_BYTES in ((0,) if nreg == 4 else (0, 8))
+                    j0 = (off % PAIR_BYTES) // 4  # first of the unit's 4 dwords per lane the read loads
+                    allowed = {4: (0,), 2: (0, 8), 1: (0, 4, 8, 12)}[nreg]
+                    assert off % PAIR_BYTES in allowed and (nreg != 1 or G.r64)
                     row = (a - G.lds_v) * PAIRS + off // PAIR_BYTES
                     assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
                     last_read[row] = max(last_read[row], phase)
                     vals = lds[row * 256:row * 256 + 256].reshape(64, 4)  # lane l: 16 B at lane*16
-                    wv.v[vd:vd + nreg] = vals[:, 2 * half:2 * half + nreg].T
+                    wv.v[vd:vd + nreg] = vals[:, j0:j0 + nreg].T
+                elif kind == "vadd":
+                    d, x, neg = f
+                    assert not _overlaps(wv.reads, x, 1), "add reads an X register whose LDS read may not have returned"
+                    wv.v[d] = wv.v[d] - wv.v[x] if neg else wv.v[d] + wv.v[x]
                 elif kind == "add":
                     d, x, neg = f
                     assert not _overlaps(wv.reads, x, 2), "add reads an X slot whose LDS read may not have returned"
@@ -240,11 +260,11 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     wv.v[t:t + 2] = np.nan  # a block sum is consumed once
         assert at_barrier in (0, WAVES), "waves disagree on the barrier count"
         phase += 1
-    acc = np.zeros((128, G.tile_cols), np.float32)
+    acc = np.zeros((G.tile_m, G.tile_cols), np.float32)
     for wv in waves:
         for c in range(NW):
-            for r in range(2):
-                acc[r:128:2, wv.w * NW + c] = wv.v[G.acc0 + 2 * c + r]
+            for r in range(RPL):
+                acc[r:G.tile_m:RPL, wv.w * NW + c] = wv.v[G.acc0 + RPL * c + r]
     return acc
 
 
@@ -256,37 +276,59 @@ def to_pairs(XT):
     return np.ascontiguousarray(q.transpose(0, 2, 1, 3).reshape(Kp // 2, Mp // 2, 4))
 
 
+def to_quads(XT):
+    """X^T [Kp][Mp] (Kp % 4 == 0) -> the k-quad layout [Kp/4][Mp][4] of the
+    64-row image (tsg_internal.h; tsg_transpose_quads_kernel)."""
+    Kp, Mp = XT.shape
+    return np.ascontiguousarray(XT.reshape(Kp // 4, 4, Mp).transpose(0, 2, 1))
+
+
 def emulate(code, wcode, X, K, N):
     assert tuple(int(x) for x in code[:2]) == MAGIC
     G = Geom(code)
-    CHUNK, TILE_COLS = G.chunk, G.tile_cols
+    CHUNK, TILE_COLS, TM = G.chunk, G.tile_cols, G.tile_m
     M = X.shape[0]
     nch = max(1, -(-K // CHUNK))
-    Mp = -(-max(M, 1) // 128) * 128
+    Mp = -(-max(M, 1) // TM) * TM
     XT = np.zeros((nch * CHUNK, Mp), np.float32)
     XT[:K, :M] = X.T
-    XP = to_pairs(XT)
+    XP = to_quads(XT) if G.r64 else to_pairs(XT)
     ntiles = len(wcode) // G.streams
     Y = np.zeros((Mp, ntiles * TILE_COLS), np.float32)
     for t in range(ntiles):
-        for m0 in range(0, Mp, 128):
-            Y[m0:m0 + 128, t * TILE_COLS:(t + 1) * TILE_COLS] = emulate_tile(code, wcode, t, XP, m0, Mp, nch)
+        for m0 in range(0, Mp, TM):
+            Y[m0:m0 + TM, t * TILE_COLS:(t + 1) * TILE_COLS] = emulate_tile(code, wcode, t, XP, m0, Mp, nch)
     return Y[:M, :N]
 
 
-def _check(tsg, O, M, K, N, s, seed, frac, W=None, width=64, waves=8):
+def _check(tsg, O, M, K, N, s, seed, frac, W=None, width=64, waves=8, rows64=False):
     W = O.gen_ternary(K, N, s, seed) if W is None else W
     t = O.tcsc_encode(W)
-    code, wcode = tsg.jit_codegen(*t.arrays, K, N, width=width, waves=waves)
+    if rows64:
+        code, wcode = tsg.jit_codegen64(*t.arrays, K, N, width=width, waves=waves)
+        assert Geom(code).r64 and Geom(code).tile_m == 64
+    else:
+        code, wcode = tsg.jit_codegen(*t.arrays, K, N, width=width, waves=waves)
     assert Geom(code).nw == width and Geom(code).waves == waves
     X = O.init_x_frac(M, K, seed + 1) if frac else O.init_x_int(M, K, seed + 1)
     b = np.linspace(-2, 3, N).astype(np.float32)
     Y = emulate(code, wcode, X, K, N) + b
     ref = O.base_tcsc(X, t, b)
     assert np.array_equal(Y.view(np.uint32), ref.view(np.uint32)), (M, K, N, s, frac)
-    # one v_pk_add_f32 per nonzero, nothing else that adds
-    n_add = sum(1 for i in range(len(code) - 1) if (int(code[i]) & 0xFFFFFD00) == 0xD3B24000
-                and (int(code[i + 1]) >> 27) & 3 == 3)
+    # one v_pk_add_f32 (64-row image: one v_add_f32 / v_sub_f32) per nonzero, nothing else that adds
+    if rows64:  # decode the region linearly from the first stream (literals are skipped by the decoder)
+        G = Geom(code)
+        pc, n_add, n_sub = int(min(wcode)) // 4, 0, 0
+        while pc < len(code):
+            kind, f, n = _decode(code, pc, G)
+            if kind == "vadd":
+                n_add += 1
+                n_sub += f[2]
+            pc += n
+        assert n_sub == len(t.arrays[3]), "one v_sub_f32 per -1 entry (comp.h:57)"
+    else:
+        n_add = sum(1 for i in range(len(code) - 1) if (int(code[i]) & 0xFFFFFD00) == 0xD3B24000
+                    and (int(code[i + 1]) >> 27) & 3 == 3)
     assert n_add == len(t.arrays[2]) + len(t.arrays[3])
 
 
@@ -337,6 +379,54 @@ def test_jit_code_far_image(tsg, oracle_mod, M, K, N, s):
         Y = emulate(code, wcode, X, K, N) + b
         ref = O.base_tcsc(X, t, b)
         assert np.array_equal(Y.view(np.uint32), ref.view(np.uint32)), (M, K, N, s, frac)
+
+
+@pytest.mark.parametrize("M,K,N,s", [(1, 1, 1, 1), (5, 70, 33, 2), (64, 200, 130, 4), (17, 300, 64, 8),
+                                     (3, 97, 9, 16), (100, 390, 40, 4)])
+@pytest.mark.parametrize("width,waves", [(64, 8), (16, 4), (8, 8)])
+def test_jit_code_64row_image(tsg, oracle_mod, M, K, N, s, width, waves):
+    """The 64-row image (one M row per lane, VOP2 v_add_f32 / v_sub_f32, k-quad
+    X^T, 192-row chunks; tsg_internal.h): emulated workgroup by workgroup,
+    every M tile of 64 rows, equal to the BaseTCSC oracle bit for bit on
+    integer and order-sensitive X, one add per nonzero."""
+    for frac in (False, True):
+        _check(tsg, oracle_mod, M, K, N, s, 5 + K + N + width, frac, width=width, waves=waves, rows64=True)
+
+
+@pytest.mark.parametrize("width,waves", [(32, 4), (16, 8), (8, 4)])
+def test_jit_code_64row_other_shapes(tsg, oracle_mod, width, waves):
+    _check(tsg, oracle_mod, 70, 500, 300, 4, 99, True, width=width, waves=waves, rows64=True)
+
+
+def test_jit_code_64row_dense_and_empty_columns(tsg, oracle_mod):
+    """Every quad read form (b32 at each row, b64 low / high, b128): dense,
+    empty, single-row and two-row columns in one W."""
+    O = oracle_mod
+    K, N = 400, 72  # width 8: stream c // 8 holds columns c..c+7, so each pattern has its own stream
+    W = np.zeros((K, N), np.int32)
+    W[:, 0] = 1                         # stream 0: dense +1 and -1 columns (b128)
+    W[:, 1] = -1
+    W[::4, 8] = 1                       # stream 1: row 0 of every quad (b32 at +0)
+    W[1::4, 16] = -1                    # b32 at +4
+    W[2::4, 24] = 1                     # b32 at +8
+    W[3::4, 32] = -1                    # b32 at +12
+    W[0::4, 40] = 1                     # rows 0, 1 in one pass (b64 at +0)
+    W[1::4, 41] = 1
+    W[2::4, 48] = -1                    # rows 2, 3 (b64 at +8)
+    W[3::4, 49] = -1
+    W[1::4, 56] = 1                     # rows 1, 2 (b128)
+    W[2::4, 57] = 1
+    W[0::4, 58] = -1                    # and rows 0, 3 of the -1 pass (b128)
+    W[3::4, 59] = -1
+    W[K - 1, 64] = 1                    # stream 8: one entry at the last row, one at the first
+    W[0, 65] = -1
+    code, _ = tsg.jit_codegen64(*O.tcsc_encode(W).arrays, K, N, width=8, waves=8)
+    ops = {int(w) & 0xFFFF0000 for w in code}
+    for op in (0xD86C0000, 0xD8EC0000, 0xD9FE0000):  # ds_read_b32 / b64 / b128 all emitted
+        assert op in ops
+    for frac in (False, True):
+        _check(tsg, O, 64, K, N, 1, 3, frac, W=W, width=8, waves=8, rows64=True)
+        _check(tsg, O, 37, K, N, 1, 4, frac, W=W, width=8, waves=8, rows64=True)
 
 
 def test_jit_width_rejected(tsg, oracle_mod):
