@@ -272,6 +272,20 @@ bool far_xt(const tsg_tcsc *h, int M)
     return long_map && 4.0 * (double)M * (double)h->K >= kFarXtBytes && 8.0 * nnz <= kFarCodeBytes;
 }
 
+// The 64-row image stages its k-quads straight from row-major X (the lane's
+// quad X[m][4q .. 4q+3] is 16 contiguous bytes) when rows start 16-B aligned
+// (K % 4 == 0, X 16-B aligned) and the per-lane offsets fit 32 bits;
+// TSG_JIT_XDIRECT=0 forces the X^T pass (A/B).
+bool x_direct(const float *dX, int M, int K)
+{
+    static const bool on = [] {
+        const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
+        return !(e && e[0] == '0');
+    }();
+    return on && K > 0 && K % 4 == 0 && ((uintptr_t)dX & 15) == 0 &&
+           (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
+}
+
 // The 64-row image (VOP2 adds, one M row per lane) or the 128-row one
 // (v_pk_add_f32, two rows per lane) for a call with M rows; BlockedTCSC runs
 // the 128-row image only.  tcsc_hip_set_tile_rows pins one.
@@ -621,8 +635,13 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     const bool r64 = pick_rows64(h, M);
     const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM, chunk = r64 ? tsg::kJit64Chunk : tsg::kJitChunk;
-    rc = ensure_work(h, M, capturing, r64);
-    if (rc) return rc;
+    // the 64-row image stages straight from row-major X (no X^T pass, no work
+    // buffer) when every row starts 16-B aligned and the offsets fit 32 bits
+    const bool direct = r64 && x_direct(dX, M, K);
+    if (!direct) {
+        rc = ensure_work(h, M, capturing, r64);
+        if (rc) return rc;
+    }
     int Mp, Kp;
     dims_for(h, M, Mp, Kp, r64);
     tsg_tcsc::JitVariant *jv = nullptr;
@@ -642,8 +661,10 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     // X^T of the previous call may still be read by its kernel on another
     // stream: this call's staging waits for it (same stream: stream order)
-    if (!capturing && h->work_used && h->work_stream != s) HIP_TRY(hipStreamWaitEvent(s, h->work_ev, 0));
-    if (K == 0) {
+    if (!direct && !capturing && h->work_used && h->work_stream != s) HIP_TRY(hipStreamWaitEvent(s, h->work_ev, 0));
+    if (direct) {
+        // no staging kernel: the dispatcher's DMA reads X itself
+    } else if (K == 0) {
         // no X at all: chain is +0; X^T stays zero
         HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
     } else if ((h->kind != tsg_tcsc::kJit ? tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s)
@@ -662,9 +683,9 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     if (h->kind == tsg_tcsc::kJit)
         pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask);
     const int lrc = h->kind == tsg_tcsc::kJit
-        ? tsg::launch_tcsc_jit(jv->mod, h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
+        ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                r64 ? h->jit64_nch : h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
-                               jv->waves, gn, gm, tmask, s, tile_m)
+                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)
@@ -674,7 +695,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         h->ring_head = (h->ring_head + 1) % tsg_tcsc::kRing;
         h->ring_count++;
     }
-    if (!capturing) {
+    if (!capturing && !direct) {
         // (a captured call's reads happen at replay time and are not tracked:
         // a replay must not overlap calls on other streams,
         // include/ternary_spgemm.h; the record of the last uncaptured call

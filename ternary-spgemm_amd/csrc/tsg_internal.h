@@ -153,7 +153,7 @@ struct JitModule {
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                     int prelu, uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask,
-                    void *stream, int tile_m = kJitTileM);
+                    void *stream, int tile_m = kJitTileM, int xrow = 0);  // xrow > 0: 64-row image staging straight from X
 int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream);
 
 // ---------------------------------------------------------------------------

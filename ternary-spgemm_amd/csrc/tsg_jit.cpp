@@ -400,7 +400,13 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         E.nop(4);  // SALU-written SGPR base -> VMEM
     };
     int vm_step = 0;  // VMEM operations (DMA pieces, code touches) issued in the current step
+    int cur_wave = 0;  // the wave whose stream is being generated
     auto dma_piece = [&](int q, int i) {
+        // 64-row image: quad rows at or past K are never staged (no entry reads
+        // them): the dispatcher may then stage straight from row-major X,
+        // whose rows end at K (tsg_jit_kernel.hip "direct X").  They are a
+        // suffix of the wave's pieces, so no M0 group loses its first piece.
+        if (r64 && 4 * ((int64_t)plan[(size_t)q].chunk * (CH / U) + (int64_t)cur_wave * kPieces + i) >= K) return;
         const uint32_t sub = m0k ? (uint32_t)(i & 3) : 0u;
         if (sub == 0) {
             E.m0_wave((uint32_t)(q % kJitRing) * kBufBytes + (uint32_t)i * kPairBytes);
@@ -443,6 +449,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         for (int w = 0; w < streams; w++) {
             while (code.size() % 64) E.nop();  // 256-B aligned stream start
             img.wcode[(size_t)t * streams + w] = E.pos_bytes();
+            cur_wave = w;
             n0 = t * tile_cols + w * nw;
             std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
@@ -710,12 +717,12 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream)
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
                     uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask, void *stream,
-                    int tile_m)
+                    int tile_m, int xrow)
 {
     int mtiles = Mp / tile_m, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
-                      (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask};
+                      (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask, (void *)&xrow};
     hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.function, (unsigned)(mtiles * ntiles), 1, 1,
                                          (unsigned)waves * 64u, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;

@@ -142,7 +142,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
-    int tmask)
+    int tmask, int xrow)
 {
     __shared__ __attribute__((aligned(16))) char lds[kJRing * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -184,19 +184,29 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
     // here (never negative: pr >= i and a pair row of X^T is >= 1 KiB)
     const uint32_t m0k = (hdr[7] & kJM0kFlag) ? 1u : 0u;
     uint32_t off[kJPieces];
+    // Direct X (64-row image, xrow > 0 floats per row of X): the lane's quad
+    // X[m][4q .. 4q+3] is 16 contiguous bytes of row-major X, so the pieces
+    // stage straight from X -- no X^T pass.  Rows past M read row M-1 (their
+    // results are never stored); quads at or past K are never staged (the
+    // generated code omits those pieces).  The chunk base starts 3 KiB below X
+    // so that off[i] stays non-negative after the m0k subtraction.
+    const bool direct = kJRows64 && xrow > 0;
+    const uint32_t xrow_b = (uint32_t)xrow * 4u, mrow = (uint32_t)min(m0 + lane, M - 1);
 #pragma unroll
     for (int i = 0; i < kJPieces; i++) {
         const uint32_t pr = (uint32_t)(wave * kJPieces + i);
-        off[i] = (pr * ((uint32_t)Mp / kJRowsPerLane) + (uint32_t)m0 / kJRowsPerLane + (uint32_t)lane) * 16u -
+        off[i] = (direct ? mrow * xrow_b + pr * 16u + 3072u
+                         : (pr * ((uint32_t)Mp / kJRowsPerLane) + (uint32_t)m0 / kJRowsPerLane + (uint32_t)lane) * 16u) -
                  m0k * (uint32_t)(i & 3) * 1024u;
     }
+    const uint64_t xbase = (uint64_t)(uintptr_t)XT - (direct ? 3072u : 0u);
     const uint32_t wb = (uint32_t)(wave * kJPieces) * 1024u;  // s83
     // code touch (one dword per 128-B line of the stream ahead, into L2): only
     // workgroups with (mt & tmask) == 0 spread it over the lines; the others
     // load one line 64 times (one request) -- the M tiles that run the same
     // stream share what one of them touched (tsg_capi.cpp pick_jit_map)
     const uint32_t l128 = (mt & tmask) == 0 ? (uint32_t)lane * 128u : 0u;
-    const uint32_t stride = (uint32_t)kJChunk * (uint32_t)Mp * 4u;
+    const uint32_t stride = direct ? (uint32_t)kJChunk * 4u : (uint32_t)kJChunk * (uint32_t)Mp * 4u;
 
 #define TSG_JIT_CALL(...)                                                                           \
     asm volatile("s_getpc_b64 s[94:95]\n"                                                           \
@@ -206,7 +216,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
                  "s_setpc_b64 %[cp]\n"                                                              \
                  ".Ljb%=:"                                                                          \
                  : __VA_ARGS__                                                                      \
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(XT), "{s82}"(stride), "{s83}"(wb), \
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(xbase), "{s82}"(stride), "{s83}"(wb), \
                    TSG_JIT_IN                                                                       \
                  : TSG_JIT_CLOBBERS)
 #if TSG_JIT_ROWS64  // one accumulator VGPR per column (acc0 = v116; 4 waves: v122)

@@ -114,6 +114,7 @@ const Knob kKnobs[] = {
     {"TSG_JIT_NW", "64 | 32 | 16 | 8", [](const char *v) { return one_of(v, {"64", "32", "16", "8"}); }},
     {"TSG_JIT_WAVES", "8 | 4", [](const char *v) { return one_of(v, {"8", "4"}); }},
     {"TSG_JIT_FAR", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
+    {"TSG_JIT_XDIRECT", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_NOALIGN", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_GN", "1..1024", [](const char *v) { return int_in(v, 1, 1024); }},
     {"TSG_JIT_GM", "1..1024", [](const char *v) { return int_in(v, 1, 1024); }},

@@ -126,3 +126,28 @@ def test_rows64_full_y_configs2_kn(tsg, oracle_mod, M):
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or len(os.sched_getaffinity(0)))))
     assert _bits_eq(h.gemm(X, b), O.base_tcsc(X, t, b, threads=threads))
     h.close()
+
+
+@pytest.mark.parametrize("M,K", [(1, 1024), (64, 4096), (130, 1000), (37, 192 * 3), (70, 196)])
+def test_rows64_direct_x_and_staged(tsg, oracle_mod, M, K):
+    """The 64-row image stages its quads straight from row-major X when the
+    rows are 16-B aligned (tsg_jit_kernel.hip "direct X": no X^T pass), and
+    through the k-quad X^T otherwise: X at a 4-byte offset takes the staged
+    path.  Both bit-exact against the oracle (rows past M read row M-1 and are
+    dropped; quads past K are never staged)."""
+    import torch
+    O = oracle_mod
+    N = 333
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, M + K))
+    h = _handle(tsg, t, K, N)
+    Xh = O.init_x_frac(M, K, 21)
+    b = torch.linspace(-2, 2, N).cuda()
+    ref = O.base_tcsc(Xh, t, b.cpu().numpy())
+    buf = torch.empty(M * K + 4, device="cuda")
+    for shift in (0, 1):  # 0: 16-B aligned (direct when K % 4 == 0); 1: 4-byte offset (staged)
+        X = buf[shift:shift + M * K].view(M, K)
+        X.copy_(torch.from_numpy(Xh))
+        Y = h.gemm_torch(X, b)
+        torch.cuda.synchronize()
+        assert _bits_eq(Y.cpu().numpy(), ref), (M, K, shift)
+    h.close()
