@@ -14,6 +14,8 @@ TSG_JIT_WAVES=4 timeout -k 10 300 python scripts/rows64_ab.py --modes jit64 --wi
 rc=$?; echo "ab 4w rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/rows64_ab_$TAG.err; exit $rc; }
 timeout -k 10 300 python scripts/rows64_ab.py --modes jit64 --widths 32,16,8 --M 32,64,128,256,512 >> gpurun_out/rows64_ab_$TAG.jsonl 2>> gpurun_out/rows64_ab_$TAG.err
 rc=$?; echo "ab 8w rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/rows64_ab_$TAG.err; exit $rc; }
+TSG_JIT_XDIRECT=0 timeout -k 10 300 python scripts/rows64_ab.py --modes jit64 --M 32,64,128,512 >> gpurun_out/rows64_ab_$TAG.jsonl 2>> gpurun_out/rows64_ab_$TAG.err
+rc=$?; echo "ab staged rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/rows64_ab_$TAG.err; exit $rc; }
 timeout -k 10 300 python scripts/rows64_ab.py --K 1024 --N 4096 --M 1,8,16,32,64,128 >> gpurun_out/rows64_ab_$TAG.jsonl 2>> gpurun_out/rows64_ab_$TAG.err
 rc=$?; echo "ab c0 rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/rows64_ab_$TAG.err; exit $rc; }
 timeout -k 10 300 python scripts/rows64_ab.py --K 4096 --N 4096 --M 256,512,1024 --modes jit128,jit64 >> gpurun_out/rows64_ab_$TAG.jsonl 2>> gpurun_out/rows64_ab_$TAG.err
@@ -22,6 +24,7 @@ python3 - gpurun_out/rows64_ab_$TAG.jsonl <<'PY'
 import json, sys
 for ln in open(sys.argv[1]):
     d = json.loads(ln)
+    d["waves_env"] = d.get("waves_env") or d.get("xdirect_env")
     cells = [f"{k}={v['kernel_ms']*1e3:.1f}us({v['width']}x{v['waves']}){'' if v['bit_identical'] else ' MISMATCH'}"
              for k, v in d.items() if isinstance(v, dict)]
     print(d["M"], d["K"], d["N"], d.get("waves_env"), " ".join(cells))

@@ -58,7 +58,8 @@ for M in (int(v) for v in a.M.split(",")):
     # order-sensitive X: mantissas over an exponent spread (every partial sum rounds)
     X = (torch.randint(-(1 << 23), 1 << 23, (M, a.K), generator=g, device="cuda", dtype=torch.int32).float()
          * torch.exp2(-torch.randint(0, 24, (M, a.K), generator=g, device="cuda").float()))
-    out = {"M": M, "K": a.K, "N": a.N, "s": a.s, "waves_env": os.environ.get("TSG_JIT_WAVES")}
+    out = {"M": M, "K": a.K, "N": a.N, "s": a.s, "waves_env": os.environ.get("TSG_JIT_WAVES"),
+           "xdirect_env": os.environ.get("TSG_JIT_XDIRECT")}
     ref = None
     for mode in a.modes.split(","):
         for w in ([0] if mode == "ell" else [int(x) for x in a.widths.split(",")]):
