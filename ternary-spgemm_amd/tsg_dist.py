@@ -45,9 +45,27 @@ def shard_widths(N: int, world: int) -> List[int]:
     return [b - a for a, b in (column_shard(N, world, r) for r in range(world))]
 
 
+_MASK64 = (1 << 64) - 1
+
+
+def _mix64(z: int) -> int:
+    """splitmix64's output finaliser (a bijection of 64-bit words)."""
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _MASK64
+    return z ^ (z >> 31)
+
+
 def block_seed(seed: int, j: int) -> int:
-    """Seed of column block j of a weak-scaled W (block 0 keeps `seed`)."""
-    return (int(seed) + j * _GOLDEN64) & ((1 << 64) - 1)
+    """Seed of column block j of a weak-scaled W (block 0 keeps `seed`).
+
+    The generator (tsg_gen_tcsc) is a splitmix64 stream whose state advances
+    by the golden-ratio constant per draw, so a seed of the form seed + j *
+    golden would start block j's stream j draws into block 0's -- nearly the
+    same matrix, shifted (tests/test_gpu_configs4.py caught it).  Blocks j > 0
+    start from a hashed state instead."""
+    if j == 0:
+        return int(seed) & _MASK64
+    return _mix64((int(seed) + j * 0xD1B54A32D192ED03) & _MASK64)
 
 
 class ShardedTCSC:
