@@ -117,10 +117,13 @@ __global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *_
     }
 }
 
-// X [M][K] -> the k-quad layout of the 64-row image (tsg_internal.h):
-// XQ[(q * Mp + m) * 4 + j] = X[m][4q + j], zero past M or K.  A 64 x 64 tile
-// of X is read along k (coalesced rows) into LDS, then written as 16 quad
-// rows of 64 float4 (1 KiB each, coalesced).
+// X [M][K] -> the blocked k-quad layout of the 64-row image (tsg_internal.h):
+// the 1-KiB piece pr = 4 qg + rg of (chunk c, M tile t) at ((c * Mt + t) * 48
+// + pr) KiB holds, in 16-B lane slot j, X[64 t + 16 rg + j % 16][4 (48 c + 4 qg
+// + j / 16) .. +3] -- zero past M or K -- so the kernel's DMA pieces are
+// coalesced 1-KiB reads.  A 64 x 64 tile of X (64 rows, 16 quads = 4 quad
+// groups of one chunk) is read along k (coalesced rows) into LDS, then written
+// as 16 whole pieces.
 template <bool VEC>
 __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *__restrict__ X,
                                                                   float *__restrict__ XQ, int M, int K,
@@ -149,14 +152,17 @@ __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *_
         }
     }
     __syncthreads();
-    // 16 quads x 64 M rows of float4 per tile: 4 per thread, lane = M row
-    const int ml = threadIdx.x & 63, ql0 = threadIdx.x >> 6;  // 64 x 4
+    // thread t writes lane slot j = t % 64 of piece (quad group i, row group t / 64):
+    // row 16 rg + j % 16, quad 4 qg + j / 16 -- 256 threads = 4 whole pieces per i
+    const int j = threadIdx.x & 63, rg = threadIdx.x >> 6, ml = rg * 16 + (j & 15);
+    const int c = k0 / 192, mt = m0 >> 6, Mt = Mp >> 6;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const int ql = ql0 + 4 * i, q = (k0 >> 2) + ql;
-        if (4 * q >= Kp) continue;
-        const int kk = 4 * ql;
-        *reinterpret_cast<float4 *>(XQ + ((size_t)q * Mp + (size_t)m0 + ml) * 4) =
+        const int qgl = i, kk = 16 * qgl + 4 * (j >> 4);   // k within the tile
+        const int qg = ((k0 % 192) >> 4) + qgl;             // quad group within the chunk (0..11)
+        if (k0 + 16 * qgl >= Kp) continue;
+        const size_t piece = ((size_t)c * Mt + mt) * 48 + (size_t)(4 * qg + rg);
+        *reinterpret_cast<float4 *>(XQ + piece * 256 + (size_t)j * 4) =
             make_float4(tile[ml][kk], tile[ml][kk + 1], tile[ml][kk + 2], tile[ml][kk + 3]);
     }
 }
@@ -331,9 +337,9 @@ int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int 
 
 int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, void *stream)
 {
-    // Mp is a multiple of 64 (the 64-row image's M tile) and Kp of 192: the
-    // 64 x 64 tiles cover [0, Kp) x [0, Mp) exactly
-    if (Mp % 64 || Kp % 64) return -1;
+    // Mp is a multiple of 64 (the 64-row image's M tile) and Kp of 192 (its
+    // chunk): the 64 x 64 tiles cover [0, Kp) x [0, Mp) exactly, three per chunk
+    if (Mp % 64 || Kp % 192) return -1;
     dim3 grid((unsigned)(Kp / 64), (unsigned)(Mp / 64));
     if (K % 4 == 0 && ((uintptr_t)X & 15) == 0)
         hipLaunchKernelGGL(tsg_transpose_quads_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, X, XQ, M, K,

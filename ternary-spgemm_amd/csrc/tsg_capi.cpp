@@ -272,17 +272,18 @@ bool far_xt(const tsg_tcsc *h, int M)
     return long_map && 4.0 * (double)M * (double)h->K >= kFarXtBytes && 8.0 * nnz <= kFarCodeBytes;
 }
 
-// The 64-row image stages its k-quads straight from row-major X (the lane's
-// quad X[m][4q .. 4q+3] is 16 contiguous bytes) when rows start 16-B aligned
-// (K % 4 == 0, X 16-B aligned) and the per-lane offsets fit 32 bits;
-// TSG_JIT_XDIRECT=0 forces the X^T pass (A/B).
+// The 64-row image stages its pieces straight from row-major X (16 rows x
+// 64 contiguous bytes each; tsg_internal.h) when rows start 16-B aligned (X
+// 16-B aligned, K % 4 == 0), no piece straddles K (K % 16 == 0: pieces at or
+// past K are omitted, so nothing reads past a row's end) and the per-lane
+// offsets fit 32 bits; TSG_JIT_XDIRECT=0 forces the staged copy (A/B).
 bool x_direct(const float *dX, int M, int K)
 {
     static const bool on = [] {
         const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
         return !(e && e[0] == '0');
     }();
-    return on && K > 0 && K % 4 == 0 && ((uintptr_t)dX & 15) == 0 &&
+    return on && K > 0 && K % 16 == 0 && ((uintptr_t)dX & 15) == 0 &&
            (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
 }
 

@@ -213,7 +213,13 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     assert rem == 0 and 0 <= j < nch
                     dst = wv.m0 + off  # the offset applies to the LDS address too
                     assert dst % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
-                    data = XP[j * PAIRS + pr, m0 // RPL:m0 // RPL + 64].reshape(-1).copy()
+                    if G.r64:  # blocked k-quad piece pr = 4 qg + rg: lane slot l = row 16 rg + l % 16, quad 4 qg + l / 16
+                        qg, rg = divmod(pr, 4)
+                        lanes = np.arange(64)
+                        q = j * PAIRS + 4 * qg + lanes // 16
+                        data = XP[q, m0 + 16 * rg + lanes % 16].reshape(-1).copy()
+                    else:
+                        data = XP[j * PAIRS + pr, m0 // RPL:m0 // RPL + 64].reshape(-1).copy()
                     wv.pending.append([(dst, data, phase)])
                 elif kind == "wait_vm":  # loads return in order: all but the newest f[0] land
                     n_land = max(len(wv.pending) - f[0], 0)
@@ -231,16 +237,31 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     vd, a, off, nreg = f
                     assert not _overlaps(wv.reads, vd, nreg), "X slot reloaded before its previous read was waited for"
                     wv.reads.append((vd, nreg))
-                    assert G.lds_v <= a < G.lds_v + NBUF and off // PAIR_BYTES < PAIRS
+                    assert G.lds_v <= a < G.lds_v + NBUF
                     assert 8 <= vd and vd + nreg <= 8 + 4 * G.xslots and (vd - 8) % 4 == 0
-                    j0 = (off % PAIR_BYTES) // 4  # first of the unit's 4 dwords per lane the read loads
                     allowed = {4: (0,), 2: (0, 8), 1: (0, 4, 8, 12)}[nreg]
-                    assert off % PAIR_BYTES in allowed and (nreg != 1 or G.r64)
-                    row = (a - G.lds_v) * PAIRS + off // PAIR_BYTES
-                    assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
-                    last_read[row] = max(last_read[row], phase)
-                    vals = lds[row * 256:row * 256 + 256].reshape(64, 4)  # lane l: 16 B at lane*16
-                    wv.v[vd:vd + nreg] = vals[:, j0:j0 + nreg].T
+                    buf = a - G.lds_v
+                    if G.r64:
+                        # blocked k-quad layout: lane l's base (dispatcher) = buffer +
+                        # (l / 16) KiB + (l % 16) * 16; quad q at (q / 4) * 4 KiB + (q % 4) * 256
+                        sub = off % 256
+                        assert sub in allowed and off // 4096 < PAIRS // 4 and (off % 4096) // 256 < 4
+                        lanes = np.arange(64)
+                        addr = buf * BUF_BYTES + (lanes // 16) * 1024 + (lanes % 16) * 16 + off
+                        pieces = np.unique(addr // PAIR_BYTES)
+                        assert len(pieces) == 4 and all(0 <= landed[p] < phase for p in pieces), \
+                            "LDS read of data not yet landed before a barrier"
+                        for p in pieces:
+                            last_read[p] = max(last_read[p], phase)
+                        wv.v[vd:vd + nreg] = np.stack([lds[addr // 4 + t] for t in range(nreg)])
+                    else:
+                        assert off // PAIR_BYTES < PAIRS and off % PAIR_BYTES in allowed and nreg != 1
+                        j0 = (off % PAIR_BYTES) // 4  # first of the unit's 4 dwords per lane the read loads
+                        row = buf * PAIRS + off // PAIR_BYTES
+                        assert 0 <= landed[row] < phase, "LDS read of data not yet landed before a barrier"
+                        last_read[row] = max(last_read[row], phase)
+                        vals = lds[row * 256:row * 256 + 256].reshape(64, 4)  # lane l: 16 B at lane*16
+                        wv.v[vd:vd + nreg] = vals[:, j0:j0 + nreg].T
                 elif kind == "vadd":
                     d, x, neg = f
                     assert not _overlaps(wv.reads, x, 1), "add reads an X register whose LDS read may not have returned"
@@ -277,8 +298,9 @@ def to_pairs(XT):
 
 
 def to_quads(XT):
-    """X^T [Kp][Mp] (Kp % 4 == 0) -> the k-quad layout [Kp/4][Mp][4] of the
-    64-row image (tsg_internal.h; tsg_transpose_quads_kernel)."""
+    """X^T [Kp][Mp] (Kp % 4 == 0) -> quads [Kp/4][Mp][4]: entry [q][m] is the
+    16 B X[m][4q .. 4q+3] (the unit the 64-row image's blocked layout moves;
+    emulate_tile gathers its DMA pieces from it)."""
     Kp, Mp = XT.shape
     return np.ascontiguousarray(XT.reshape(Kp // 4, 4, Mp).transpose(0, 2, 1))
 
