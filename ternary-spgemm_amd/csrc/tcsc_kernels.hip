@@ -118,10 +118,10 @@ __global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *_
 }
 
 // X [M][K] -> the blocked k-quad layout of the 64-row image (tsg_internal.h):
-// the 1-KiB piece pr = 4 qg + rg of (chunk c, M tile t) at ((c * Mt + t) * 48
-// + pr) KiB holds, in 16-B lane slot j, X[64 t + 16 rg + j % 16][4 (48 c + 4 qg
-// + j / 16) .. +3] -- zero past M or K -- so the kernel's DMA pieces are
-// coalesced 1-KiB reads.  A 64 x 64 tile of X (64 rows, 16 quads = 4 quad
+// the 1-KiB piece pr = 8 qg + rg of (chunk c, M tile t) at ((c * Mt + t) * 48
+// + pr) KiB holds, in 16-B lane slot j, X[64 t + 8 rg + j % 8][4 (48 c + 8 qg
+// + j / 8) .. +3] -- zero past M or K -- so the kernel's DMA pieces are
+// coalesced 1-KiB reads.  A 64 x 64 tile of X (64 rows, 16 quads = 2 quad
 // groups of one chunk) is read along k (coalesced rows) into LDS, then written
 // as 16 whole pieces.
 template <bool VEC>
@@ -152,16 +152,17 @@ __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *_
         }
     }
     __syncthreads();
-    // thread t writes lane slot j = t % 64 of piece (quad group i, row group t / 64):
-    // row 16 rg + j % 16, quad 4 qg + j / 16 -- 256 threads = 4 whole pieces per i
-    const int j = threadIdx.x & 63, rg = threadIdx.x >> 6, ml = rg * 16 + (j & 15);
+    // thread t writes lane slot j = t % 64 of the tile's piece p = 4 i + t / 64
+    // (quad group p / 8, row group p % 8): row 8 rg + j % 8, quad 8 qg + j / 8
+    // -- 256 threads = 4 whole pieces per i, 16 per tile
+    const int j = threadIdx.x & 63;
     const int c = k0 / 192, mt = m0 >> 6, Mt = Mp >> 6;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const int qgl = i, kk = 16 * qgl + 4 * (j >> 4);   // k within the tile
-        const int qg = ((k0 % 192) >> 4) + qgl;             // quad group within the chunk (0..11)
-        if (k0 + 16 * qgl >= Kp) continue;
-        const size_t piece = ((size_t)c * Mt + mt) * 48 + (size_t)(4 * qg + rg);
+        const int p = 4 * i + (threadIdx.x >> 6), qgl = p >> 3, rg = p & 7, ml = rg * 8 + (j & 7);
+        const int kk = 32 * qgl + 4 * (j >> 3);             // k within the tile
+        const int qg = ((k0 % 192) >> 5) + qgl;             // quad group within the chunk (0..5)
+        const size_t piece = ((size_t)c * Mt + mt) * 48 + (size_t)(8 * qg + rg);
         *reinterpret_cast<float4 *>(XQ + piece * 256 + (size_t)j * 4) =
             make_float4(tile[ml][kk], tile[ml][kk + 1], tile[ml][kk + 2], tile[ml][kk + 3]);
     }

@@ -105,12 +105,14 @@ namespace {
 // Largest M the automatic choice sends to the small-M (ELL) kernel (see
 // pick_ell_variant), the variant with 8-row tiles, and the M up to which
 // 8-row tiles are used.
-constexpr int kEllAutoMaxM = 64;
+constexpr int kEllAutoMaxM = 32;
 constexpr int kEllAutoMaxMChunked = 32;
 constexpr int kEllTile8 = 2;
 constexpr int kEllMidM = 32;
 constexpr int64_t kEllPcRowsMaxMN = 32768;
 constexpr int kEllStarvedMaxM = 1024;
+// Largest M the automatic choice sends to the 64-row image (pick_rows64)
+constexpr int kRows64AutoMaxM = 512;
 constexpr int64_t kJitFullWgs = 230;
 constexpr int64_t kJitOneRoundWgs = 256;  // one jit workgroup per CU (144 KiB of LDS)
 constexpr double kFarXtBytes = 768.0 * 1024 * 1024;  // X^T >= 3x the 256 MiB Infinity Cache
@@ -272,10 +274,10 @@ bool far_xt(const tsg_tcsc *h, int M)
     return long_map && 4.0 * (double)M * (double)h->K >= kFarXtBytes && 8.0 * nnz <= kFarCodeBytes;
 }
 
-// The 64-row image stages its pieces straight from row-major X (16 rows x
-// 64 contiguous bytes each; tsg_internal.h) when rows start 16-B aligned (X
-// 16-B aligned, K % 4 == 0), no piece straddles K (K % 16 == 0: pieces at or
-// past K are omitted, so nothing reads past a row's end) and the per-lane
+// The 64-row image stages its pieces straight from row-major X (8 rows x one
+// 128-B line each; tsg_internal.h) when rows start 16-B aligned (X 16-B
+// aligned, K % 4 == 0), no piece straddles K (K % 32 == 0: pieces at or past
+// K are omitted, so nothing reads past a row's end) and the per-lane
 // offsets fit 32 bits; TSG_JIT_XDIRECT=0 forces the staged copy (A/B).
 bool x_direct(const float *dX, int M, int K)
 {
@@ -283,18 +285,30 @@ bool x_direct(const float *dX, int M, int K)
         const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
         return !(e && e[0] == '0');
     }();
-    return on && K > 0 && K % 16 == 0 && ((uintptr_t)dX & 15) == 0 &&
+    return on && K > 0 && K % 32 == 0 && ((uintptr_t)dX & 15) == 0 &&
            (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
 }
 
 // The 64-row image (VOP2 adds, one M row per lane) or the 128-row one
-// (v_pk_add_f32, two rows per lane) for a call with M rows; BlockedTCSC runs
-// the 128-row image only.  tcsc_hip_set_tile_rows pins one.
+// (v_pk_add_f32, two rows per lane) for a call with M rows (that the small-M
+// walk does not take); BlockedTCSC runs the 128-row image only.  Measured
+// (profiles/r04d_rows64_ab.jsonl, r04d_rows64_big.jsonl; kernel / step us,
+// same box): at K = 4096, N = 16384 the 64-row image wins from M = 48 (68 vs
+// ELL 95 / 128-row 107) through M = 512 (202 / 209 vs 228 / 243; M = 64 78 /
+// 84 vs 108 / 121, M = 128 90 / 96 vs 110 / 123, M = 256 119 / 125 vs 150 /
+// 164), and configs[1] (512, 4096, 4096) by its step (107 vs 112: no X^T
+// pass); from M = 1024 the 128-row image is as fast or faster (configs[2]
+// 1314 / 1351 vs 1405 / 1411).  tcsc_hip_set_tile_rows pins one;
+// TSG_JIT_ROWS64_MAXM moves the boundary (A/B).
 bool pick_rows64(const tsg_tcsc *h, int M)
 {
-    (void)M;
+    static const int max_m = [] {
+        const char *e = tsg::knob_value("TSG_JIT_ROWS64_MAXM");
+        return e ? atoi(e) : kRows64AutoMaxM;
+    }();
     if (h->B || h->kind != tsg_tcsc::kJit) return false;
-    return h->tile_rows == 64;
+    if (h->tile_rows) return h->tile_rows == 64;
+    return M <= max_m;
 }
 
 JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64 = false)
@@ -311,6 +325,37 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64 = false)
     const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM;
     const int64_t mt = (std::max(M, 1) + tile_m - 1) / tile_m;
     const double image8 = (r64 ? 4.0 : 8.0) * (double)(h->nnz_pos + h->nnz_neg);
+    if (r64) {
+        // 64-row image: the shape with the least modelled time = rounds of
+        // one-workgroup-per-CU x the time of a workgroup, which grows with the
+        // columns a SIMD carries (width x waves / 4) scaled by density, over a
+        // fixed part (the K sweep's staging and barriers).  Fitted on one
+        // full round at K = 4096, s = 4 (profiles/r04d_rows64_ab.jsonl): 16 x 4
+        // 78 us, 32 x 4 93, 16 x 8 91, 32 x 8 110-118, 64 x 8 202 us ~ 1.15 x
+        // (48 + columns per SIMD).  A fractional round costs a whole one (M =
+        // 192: 32 x 4 on 384 workgroups 178 us; one round of 32 x 8 ~ 115).
+        // Ties go to the wider stream (fewer LDS reads per add).
+        const double dens4 = 4.0 * (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
+        JitShape pick{tsg::kJitNW, tsg::kJitWaves, false, true};
+        double best_cost = 0.0;
+        bool any = false;
+        for (int nw : tsg::kJitWidths)
+            for (int waves : {tsg::kJitWaves, 4}) {
+                if (!tsg::jit_waves_ok(nw, waves)) continue;
+                if (env_waves == 4 && nw != tsg::kJitNW && waves != 4) continue;
+                const int64_t ntile = (h->N + (int64_t)waves * nw - 1) / ((int64_t)waves * nw), wgs = mt * ntile;
+                const double image = image8 + (double)ntile * waves * h->jit_nch * 2 * (160.0 + 8.0 * tsg::kJitChunk);
+                if (nw != tsg::kJitNW && image > 2.0 * (double)(1ull << 30)) continue;
+                const double rounds = (double)((wgs + kJitOneRoundWgs - 1) / kJitOneRoundWgs);
+                const double cost = rounds * (48.0 + (double)nw * waves / 4.0 * dens4);
+                if (!any || cost < best_cost) {
+                    any = true;
+                    best_cost = cost;
+                    pick = {nw, waves, false, true};
+                }
+            }
+        return pick;
+    }
     JitShape best{tsg::kJitNW, tsg::kJitWaves}, most{tsg::kJitNW, tsg::kJitWaves};
     int64_t most_wgs = -1;
     bool full = false;
@@ -506,10 +551,10 @@ bool use_ell_pc(const tsg_tcsc *h, int v) { return v == 0 && ell_pc_available(h)
 // configs[2]'s and configs[0]'s K, N (profiles/r02u_ell_lg.txt): up to M = 8
 // the smallest M tile that holds M; up to M = 32 tiles of 8 (2 rows per lane:
 // an 8-row chunk of K = 4096 fits LDS, one stream per column); above that the
-// largest tile whose chunk holds K.  Automatic up to M = 64 when an 8-row
-// tile holds K in one chunk (ELL 98 us vs jit 123 us at M = 64, K = 4096),
-// else up to M = 32 (K = N = 16384: M = 16 0.18 vs 0.39 ms, M = 32 0.29 vs 0.39 ms,
-// M = 40 0.51 vs 0.39 ms; profiles/r03_half_tile_ab.txt); and up to M = 1024 while the
+// largest tile whose chunk holds K.  Automatic up to M = 32 (round 4: the
+// 64-row image takes 32 < M, K = 4096, N = 16384: M = 32 ELL 51 / step 58 vs
+// 59 / 65 us, M = 48 95 vs 68 us, M = 64 97 vs 78 us; K = N = 16384 M = 32
+// 0.29 vs 0.39 ms on the 128-row image, profiles/r03_half_tile_ab.txt); and up to M = 1024 while the
 // jit kernel would have at most 64 workgroups (the reference's (1000, 2048,
 // 512): 31 vs 52 us; (256, 4096, 1024): 34 vs 91 us; at 128 workgroups the
 // jit kernel wins: (1024, 1024, 1024) 32 vs 35 us;

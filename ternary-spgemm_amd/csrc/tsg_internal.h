@@ -108,18 +108,19 @@ constexpr uint32_t kJitFarFlag = 1u << 17;
 //
 // Blocked k-quad layout: a lane's unit is a quad, the 16 B X[m][4q .. 4q+3]
 // (contiguous in row-major X).  An M tile's chunk (64 rows x 192 K rows = 48
-// quads, 48 KiB) is 48 pieces of 1 KiB; piece pr = 4 qg + rg holds row group
-// rg (rows 16 rg .. 16 rg + 15) x quad group qg (quads 4 qg .. 4 qg + 3) with
-// DMA lane j carrying row 16 rg + j % 16, quad 4 qg + j / 16.  So in LDS the
-// quad q of row r sits at (q / 4) * 4 KiB + (r / 16) * 1 KiB + (q % 4) * 256 +
-// (r % 16) * 16: a lane's base (r / 16) * 1 KiB + (r % 16) * 16 plus a
-// uniform offset per quad (one ds_read_b128 loads four k rows of its row;
-// b64 / b32 for quads with 2 / 1 used rows), 16 lanes reading 256 contiguous
-// bytes (no bank conflict).  The DMA pieces read either a staged copy in the
-// same order (tsg_transpose_quads_kernel: piece (chunk c, M tile t, pr) is the
-// 1 KiB at ((c * Mt + t) * 48 + pr) KiB, coalesced) or row-major X itself
-// ("direct X": 16 rows x 64 contiguous bytes per piece, no X^T pass).  The
-// ring, the DMA issue and the register contract are the 128-row image's.
+// quads, 48 KiB) is 48 pieces of 1 KiB; piece pr = 8 qg + rg holds row group
+// rg (rows 8 rg .. 8 rg + 7) x quad group qg (quads 8 qg .. 8 qg + 7: one
+// 128-B line of each row) with DMA lane j carrying row 8 rg + j % 8, quad
+// 8 qg + j / 8.  So in LDS the quad q of row r sits at (q / 8) * 8 KiB +
+// (r / 8) * 1 KiB + (q % 8) * 128 + (r % 8) * 16: a lane's base (r / 8) * 1 KiB
+// + (r % 8) * 16 plus a uniform offset per quad (one ds_read_b128 loads four
+// k rows of its row; b64 / b32 for quads with 2 / 1 used rows), each 8 lanes
+// reading 128 contiguous bytes (no bank conflict).  The DMA pieces read
+// either a staged copy in the same order (tsg_transpose_quads_kernel: piece
+// (chunk c, M tile t, pr) is the 1 KiB at ((c * Mt + t) * 48 + pr) KiB,
+// coalesced) or row-major X itself ("direct X": 8 whole 128-B lines per
+// piece, no X^T pass).  The ring, the DMA issue and the register contract are
+// the 128-row image's.
 // Dispatchers lib/tsg_jit64_w<nw>[_4w].co (kernel tsg_jit64_kernel).
 constexpr int kJit64TileM = 64;
 constexpr int kJit64Chunk = 192;

@@ -402,13 +402,13 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     int vm_step = 0;  // VMEM operations (DMA pieces, code touches) issued in the current step
     int cur_wave = 0;  // the wave whose stream is being generated
     auto dma_piece = [&](int q, int i) {
-        // 64-row image: a piece holds quads 4 qg .. 4 qg + 3 of the chunk
+        // 64-row image: piece pr holds quads 8 (pr / 8) .. + 7 of the chunk
         // (tsg_internal.h, blocked k-quad layout); pieces whose quads all lie
         // at or past K are never staged (no entry reads them): the dispatcher
         // may then stage straight from row-major X, whose rows end at K
-        // (tsg_jit_kernel.hip "direct X", K % 16 == 0).  They are a suffix of
+        // (tsg_jit_kernel.hip "direct X", K % 32 == 0).  They are a suffix of
         // the wave's pieces, so no M0 group loses its first piece.
-        if (r64 && 16 * ((int64_t)plan[(size_t)q].chunk * (CH / 16) + ((int64_t)cur_wave * kPieces + i) / 4) >= K)
+        if (r64 && 32 * ((int64_t)plan[(size_t)q].chunk * (CH / 32) + ((int64_t)cur_wave * kPieces + i) / 8) >= K)
             return;
         const uint32_t sub = m0k ? (uint32_t)(i & 3) : 0u;
         if (sub == 0) {
@@ -486,8 +486,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     const uint32_t dst = kXSlot0 + (uint32_t)(kJitSlotRegs * (issued % S));
                     const uint32_t lb = kLdsBaseV + (uint32_t)(rq % kJitRing);
                     // 64-row image, blocked k-quad layout: quad q of the chunk at
-                    // (q / 4) * 4 KiB + (q % 4) * 256 B from the lane's base
-                    const uint32_t off = r64 ? (uint32_t)(rd.pair / 4) * 4096u + (uint32_t)(rd.pair % 4) * 256u
+                    // (q / 8) * 8 KiB + (q % 8) * 128 B from the lane's base
+                    const uint32_t off = r64 ? (uint32_t)(rd.pair / 8) * 8192u + (uint32_t)(rd.pair % 8) * 128u
                                              : (uint32_t)rd.pair * kPairBytes;
                     if (r64) {
                         const QuadRead qr = quad_read(rd.mask);

@@ -9,8 +9,9 @@ import pytest
 @pytest.mark.parametrize("shape,plan", [
     # configs[2] (the bench): 64 x 8, CU pairs on one code stream (2 x 16)
     ((4096, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(2, 16), tmask=0)),
-    # configs[1]: 16 x 4 one-round grid, code touches thinned (r03e_touch_ab.txt, r03q_mid_shape_ab.txt)
-    ((512, 4096, 4096, 4), dict(kernel="tsg_jit_kernel", width=16, waves=4, far=False, map=(4, 4), tmask=3)),
+    # configs[1]: the 64-row image, 32 x 4 one-round grid, code touches thinned (round 4:
+    # step 107 vs 112 us for the 128-row image's 16 x 4, r04d_rows64_big.jsonl)
+    ((512, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=4, far=False, map=(4, 8), tmask=3)),
     # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt)
     ((4096, 4096, 16384, 16), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=0)),
     # the reference's largest case: s = 4 far-X^T image on 1 x 32 (r03e_far_ab.txt) ...
@@ -23,8 +24,14 @@ import pytest
     # X^T too small for the far image (r03e_long_k_ab.txt) / large enough
     ((8192, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
     ((16000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
-    # 2 M tiles per stream: every tile touches (r03g_ref_cases.jsonl)
-    ((256, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=32, waves=4, far=False, map=(4, 2), tmask=0)),
+    # the 64-row image at mid M (round 4, r04d_rows64_ab.jsonl): one round of workgroups,
+    # the shape of least modelled time (tsg_capi.cpp pick_jit_shape)
+    ((256, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(4, 4), tmask=3)),
+    ((512, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=3)),
+    ((128, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=4, far=False, map=(4, 2), tmask=0)),
+    ((64, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=4, far=False, map=(4, 1), tmask=0)),
+    # M = 192: one round of 32 x 8 (192 workgroups), not 1.5 rounds of 32 x 4 (178 us measured)
+    ((192, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(4, 3), tmask=0)),
     ((1024, 4096, 1024, 4), dict(kernel="tsg_jit_kernel", width=8, waves=4, far=False, map=(4, 8), tmask=3)),
 ])
 def test_plan_matches_measured_winners(tsg, shape, plan):
@@ -36,11 +43,15 @@ def test_plan_matches_measured_winners(tsg, shape, plan):
 @pytest.mark.parametrize("M,K,N,kernel", [
     (1, 4096, 16384, "tsg_tcsc_ell_pc_kernel"),   # M = 1: producer/consumer walk
     (16, 4096, 16384, "tsg_tcsc_ell_kernel"),     # small M: the sliced-ELL walk
-    (64, 4096, 16384, "tsg_tcsc_ell_kernel"),     # up to 64 while an 8-row tile holds K
-    (96, 4096, 16384, "tsg_jit_kernel"),
+    (32, 4096, 16384, "tsg_tcsc_ell_kernel"),     # up to 32 (51 vs 59 us, r04d_rows64_ab.jsonl)
+    (33, 4096, 16384, "tsg_jit64_kernel"),        # then the 64-row image (M = 48: 68 vs 95 us)
+    (64, 4096, 16384, "tsg_jit64_kernel"),
+    (96, 4096, 16384, "tsg_jit64_kernel"),
+    (512, 4096, 16384, "tsg_jit64_kernel"),
+    (513, 4096, 16384, "tsg_jit_kernel"),         # the 128-row image from M > 512 (configs[2]: 1314 vs 1405 us)
     (32, 1024, 4096, "tsg_tcsc_ell_kernel"),      # configs[0]
     (32, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 32
-    (40, 16384, 16384, "tsg_jit_kernel"),
+    (40, 16384, 16384, "tsg_jit64_kernel"),
     (1000, 2048, 512, "tsg_tcsc_ell_kernel"),     # starved jit grid (<= 64 workgroups)
 ])
 def test_plan_small_m_kernel(tsg, M, K, N, kernel):

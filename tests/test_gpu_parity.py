@@ -98,6 +98,7 @@ def test_every_stream_width_vs_oracle(tsg, oracle_mod, width):
         t = O.tcsc_encode(W)
         h = tsg.TCSCDevice(*t.arrays, K, N)
         h.set_small_m(1)  # the weight-compiled kernel for every M (M = 1 would take the small-M kernel)
+        h.set_tile_rows(128)  # the 128-row image (the 64-row one: tests/test_gpu_rows64.py)
         h.set_jit_width(width)
         assert h.jit_width(M) == width and h.call_kernel(M) == "tsg_jit_kernel"
         b = (np.arange(N, dtype=np.float32) - N / 2) * 0.37
@@ -118,6 +119,7 @@ def test_far_image_vs_oracle(tsg, oracle_mod):
         t = O.tcsc_encode(W)
         h = tsg.TCSCDevice(*t.arrays, K, N)
         h.set_small_m(1)
+        h.set_tile_rows(128)
         h.set_jit_width(64)
         assert not h.call_far(M)  # X^T far below the Infinity Cache: the default image
         b = (np.arange(N, dtype=np.float32) - N / 3) * 0.21
@@ -161,15 +163,17 @@ def test_auto_width_small_m(tsg, oracle_mod):
                                          (1024, 1024, 4096, (32, 4)), (4096, 1024, 16384, (64, 8)),
                                          (300, 1000, 700, None)])
 def test_auto_shape_mid_m(tsg, oracle_mod, M, K, N, shape):
-    """The automatic (width, waves) shape at mid M: 4-wave workgroups where
-    they double the workgroups of a wider stream (configs[1] takes 16 x 4);
-    every launched shape bit for bit on sampled rows, and one handle switching
-    shapes call by call."""
+    """The automatic (width, waves) shape of the 128-row image at mid M (pinned:
+    the automatic choice runs the 64-row image up to M = 512): 4-wave
+    workgroups where they double the workgroups of a wider stream (configs[1]
+    on this image takes 16 x 4); every launched shape bit for bit on sampled
+    rows, and one handle switching shapes call by call."""
     import torch
     O = oracle_mod
     arrs = tsg.gen_tcsc(K, N, 4, 5)
     h = tsg.TCSCDevice(*arrs, K, N)
     h.set_small_m(1)
+    h.set_tile_rows(128)
     if shape is not None:
         assert (h.jit_width(M), h.jit_waves(M)) == shape
     b = torch.linspace(-2, 2, N, device="cuda")

@@ -92,7 +92,7 @@ def test_auto_choice_and_structural_edges(tsg, oracle_mod):
     assert h.call_kernel(1) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(4096) == "tsg_jit_kernel"
     assert h.call_kernel(4) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(5) == "tsg_tcsc_ell_kernel"
     h.set_small_m(1)
-    assert h.call_kernel(1) == "tsg_jit_kernel"
+    assert h.call_kernel(1) == "tsg_jit64_kernel"  # small M off: the 64-row weight-compiled image
     h.close()
     # empty / dense / all-zero W and K = 0 on the small-M kernel
     rng = np.random.default_rng(3)
@@ -123,14 +123,15 @@ def test_auto_choice_and_structural_edges(tsg, oracle_mod):
 def test_config3_shape_small_m(tsg, oracle_mod, M):
     """configs[2]'s K = 4096, N = 16384 at GEMV-like M (the reference sweep's
     M list, plots/run_benchmark.py:8), automatic choice (the small-M kernel up
-    to M = 64 at this K), against the oracle."""
+    to M = 32 at this K, then the 64-row weight-compiled image), against the
+    oracle."""
     import torch
     O = oracle_mod
     K, N = 4096, 16384
     arrs = tsg.gen_tcsc(K, N, 4, 42)
     h = tsg.TCSCDevice(*arrs, K, N)
-    assert h.call_kernel(M) == ("tsg_tcsc_ell_pc_kernel" if M <= 2 else "tsg_tcsc_ell_kernel" if M <= 64
-                                else "tsg_jit_kernel")
+    assert h.call_kernel(M) == ("tsg_tcsc_ell_pc_kernel" if M <= 2 else "tsg_tcsc_ell_kernel" if M <= 32
+                                else "tsg_jit64_kernel")
     Xn = O.init_x_frac(M, K, 5)
     b = np.full(N, 2.0, np.float32)
     Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()

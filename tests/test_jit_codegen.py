@@ -213,11 +213,11 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     assert rem == 0 and 0 <= j < nch
                     dst = wv.m0 + off  # the offset applies to the LDS address too
                     assert dst % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
-                    if G.r64:  # blocked k-quad piece pr = 4 qg + rg: lane slot l = row 16 rg + l % 16, quad 4 qg + l / 16
-                        qg, rg = divmod(pr, 4)
+                    if G.r64:  # blocked k-quad piece pr = 8 qg + rg: lane slot l = row 8 rg + l % 8, quad 8 qg + l / 8
+                        qg, rg = divmod(pr, 8)
                         lanes = np.arange(64)
-                        q = j * PAIRS + 4 * qg + lanes // 16
-                        data = XP[q, m0 + 16 * rg + lanes % 16].reshape(-1).copy()
+                        q = j * PAIRS + 8 * qg + lanes // 8
+                        data = XP[q, m0 + 8 * rg + lanes % 8].reshape(-1).copy()
                     else:
                         data = XP[j * PAIRS + pr, m0 // RPL:m0 // RPL + 64].reshape(-1).copy()
                     wv.pending.append([(dst, data, phase)])
@@ -243,13 +243,13 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     buf = a - G.lds_v
                     if G.r64:
                         # blocked k-quad layout: lane l's base (dispatcher) = buffer +
-                        # (l / 16) KiB + (l % 16) * 16; quad q at (q / 4) * 4 KiB + (q % 4) * 256
-                        sub = off % 256
-                        assert sub in allowed and off // 4096 < PAIRS // 4 and (off % 4096) // 256 < 4
+                        # (l / 8) KiB + (l % 8) * 16; quad q at (q / 8) * 8 KiB + (q % 8) * 128
+                        sub = off % 128
+                        assert sub in allowed and off // 8192 < PAIRS // 8
                         lanes = np.arange(64)
-                        addr = buf * BUF_BYTES + (lanes // 16) * 1024 + (lanes % 16) * 16 + off
+                        addr = buf * BUF_BYTES + (lanes // 8) * 1024 + (lanes % 8) * 16 + off
                         pieces = np.unique(addr // PAIR_BYTES)
-                        assert len(pieces) == 4 and all(0 <= landed[p] < phase for p in pieces), \
+                        assert len(pieces) == 8 and all(0 <= landed[p] < phase for p in pieces), \
                             "LDS read of data not yet landed before a barrier"
                         for p in pieces:
                             last_read[p] = max(last_read[p], phase)
