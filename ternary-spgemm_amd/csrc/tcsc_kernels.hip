@@ -117,14 +117,14 @@ __global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *_
     }
 }
 
-// X [M][K] -> the blocked k-quad layout of the 64-row image (tsg_internal.h):
-// the 1-KiB piece pr = 8 qg + rg of (chunk c, M tile t) at ((c * Mt + t) * 48
-// + pr) KiB holds, in 16-B lane slot j, X[64 t + 8 rg + j % 8][4 (48 c + 8 qg
-// + j / 8) .. +3] -- zero past M or K -- so the kernel's DMA pieces are
-// coalesced 1-KiB reads.  A 64 x 64 tile of X (64 rows, 16 quads = 2 quad
-// groups of one chunk) is read along k (coalesced rows) into LDS, then written
-// as 16 whole pieces.
-template <bool VEC>
+// X [M][K] -> the blocked k-quad layout of the 64-row image (tsg_internal.h),
+// PR rows per piece (16 or 8) and Q = 64 / PR quads: the 1-KiB piece pr = Q qg
+// + rg of (chunk c, M tile t) at ((c * Mt + t) * 48 + pr) KiB holds, in 16-B
+// lane slot j, X[64 t + PR rg + j % PR][4 (48 c + Q qg + j / PR) .. +3] -- zero
+// past M or K -- so the kernel's DMA pieces are coalesced 1-KiB reads.  A 64 x
+// 64 tile of X (64 rows x 16 quads of one chunk) is read along k (coalesced
+// rows) into LDS, then written as 16 whole pieces.
+template <bool VEC, int PR>
 __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *__restrict__ X,
                                                                   float *__restrict__ XQ, int M, int K,
                                                                   int Mp, int Kp)
@@ -153,16 +153,17 @@ __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *_
     }
     __syncthreads();
     // thread t writes lane slot j = t % 64 of the tile's piece p = 4 i + t / 64
-    // (quad group p / 8, row group p % 8): row 8 rg + j % 8, quad 8 qg + j / 8
+    // (quad group p / Q, row group p % Q): row PR rg + j % PR, quad Q qg + j / PR
     // -- 256 threads = 4 whole pieces per i, 16 per tile
+    constexpr int Q = 64 / PR;
     const int j = threadIdx.x & 63;
     const int c = k0 / 192, mt = m0 >> 6, Mt = Mp >> 6;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const int p = 4 * i + (threadIdx.x >> 6), qgl = p >> 3, rg = p & 7, ml = rg * 8 + (j & 7);
-        const int kk = 32 * qgl + 4 * (j >> 3);             // k within the tile
-        const int qg = ((k0 % 192) >> 5) + qgl;             // quad group within the chunk (0..5)
-        const size_t piece = ((size_t)c * Mt + mt) * 48 + (size_t)(8 * qg + rg);
+        const int p = 4 * i + (threadIdx.x >> 6), qgl = p / Q, rg = p % Q, ml = rg * PR + (j % PR);
+        const int kk = 4 * (Q * qgl + j / PR);               // k within the tile
+        const int qg = (k0 % 192) / (4 * Q) + qgl;           // quad group within the chunk
+        const size_t piece = ((size_t)c * Mt + mt) * 48 + (size_t)(Q * qg + rg);
         *reinterpret_cast<float4 *>(XQ + piece * 256 + (size_t)j * 4) =
             make_float4(tile[ml][kk], tile[ml][kk + 1], tile[ml][kk + 2], tile[ml][kk + 3]);
     }
@@ -336,18 +337,23 @@ int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, void *stream)
+int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream)
 {
     // Mp is a multiple of 64 (the 64-row image's M tile) and Kp of 192 (its
     // chunk): the 64 x 64 tiles cover [0, Kp) x [0, Mp) exactly, three per chunk
     if (Mp % 64 || Kp % 192) return -1;
     dim3 grid((unsigned)(Kp / 64), (unsigned)(Mp / 64));
-    if (K % 4 == 0 && ((uintptr_t)X & 15) == 0)
-        hipLaunchKernelGGL(tsg_transpose_quads_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, X, XQ, M, K,
-                           Mp, Kp);
-    else
-        hipLaunchKernelGGL(tsg_transpose_quads_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, X, XQ, M, K,
-                           Mp, Kp);
+    const bool vec = K % 4 == 0 && ((uintptr_t)X & 15) == 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (piece_rows == 16) {
+        if (vec) hipLaunchKernelGGL((tsg_transpose_quads_kernel<true, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
+        else hipLaunchKernelGGL((tsg_transpose_quads_kernel<false, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
+    } else if (piece_rows == 8) {
+        if (vec) hipLaunchKernelGGL((tsg_transpose_quads_kernel<true, 8>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
+        else hipLaunchKernelGGL((tsg_transpose_quads_kernel<false, 8>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
+    } else {
+        return -1;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

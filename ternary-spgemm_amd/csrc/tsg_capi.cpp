@@ -47,6 +47,7 @@ struct tsg_tcsc {
     // call with an M that picks them (or tcsc_hip_reserve)
     struct JitVariant {
         int nw = 0, waves = 0, Npad = 0;
+        int piece_rows = 0;               // 64-row image: rows per DMA piece (its X^T layout)
         tsg::JitModule mod;               // dispatcher + generated code, loaded
         uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
         int64_t code_bytes = 0, wcode_words = 0;
@@ -274,18 +275,19 @@ bool far_xt(const tsg_tcsc *h, int M)
     return long_map && 4.0 * (double)M * (double)h->K >= kFarXtBytes && 8.0 * nnz <= kFarCodeBytes;
 }
 
-// The 64-row image stages its pieces straight from row-major X (8 rows x one
-// 128-B line each; tsg_internal.h) when rows start 16-B aligned (X 16-B
-// aligned, K % 4 == 0), no piece straddles K (K % 32 == 0: pieces at or past
-// K are omitted, so nothing reads past a row's end) and the per-lane
+// The 64-row image stages its pieces straight from row-major X (PR rows x
+// 1024 / PR contiguous bytes each; tsg_internal.h) when rows start 16-B
+// aligned (X 16-B aligned, K % 4 == 0), no piece straddles K (K % (256 / PR)
+// == 0: pieces at or past K are omitted, so nothing reads past a row's end)
+// and the per-lane
 // offsets fit 32 bits; TSG_JIT_XDIRECT=0 forces the staged copy (A/B).
-bool x_direct(const float *dX, int M, int K)
+bool x_direct(const float *dX, int M, int K, int piece_rows)
 {
     static const bool on = [] {
         const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
         return !(e && e[0] == '0');
     }();
-    return on && K > 0 && K % 32 == 0 && ((uintptr_t)dX & 15) == 0 &&
+    return on && K > 0 && piece_rows > 0 && K % (256 / piece_rows) == 0 && ((uintptr_t)dX & 15) == 0 &&
            (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
 }
 
@@ -520,6 +522,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
     v.nw = nw;
     v.waves = waves;
     v.Npad = img.Npad;
+    v.piece_rows = img.piece_rows;
     v.code_bytes = (int64_t)img.code.size() * 4;
     v.wcode_words = (int64_t)img.wcode.size();
     (r64 ? h->jit64_nch : h->jit_nch) = img.nch;
@@ -681,13 +684,6 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     const bool r64 = pick_rows64(h, M);
     const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM, chunk = r64 ? tsg::kJit64Chunk : tsg::kJitChunk;
-    // the 64-row image stages straight from row-major X (no X^T pass, no work
-    // buffer) when every row starts 16-B aligned and the offsets fit 32 bits
-    const bool direct = r64 && x_direct(dX, M, K);
-    if (!direct) {
-        rc = ensure_work(h, M, capturing, r64);
-        if (rc) return rc;
-    }
     int Mp, Kp;
     dims_for(h, M, Mp, Kp, r64);
     tsg_tcsc::JitVariant *jv = nullptr;
@@ -705,6 +701,13 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         if ((int64_t)Mp * chunk * 4 >= (1ll << 31) || wgs * jv->waves * 64 >= (1ll << 32))
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " is too large for one jit launch; split the rows");
     }
+    // the 64-row image stages straight from row-major X (no X^T pass, no work
+    // buffer) when every row starts 16-B aligned and the offsets fit 32 bits
+    const bool direct = r64 && x_direct(dX, M, K, jv->piece_rows);
+    if (!direct) {
+        rc = ensure_work(h, M, capturing, r64);
+        if (rc) return rc;
+    }
     // X^T of the previous call may still be read by its kernel on another
     // stream: this call's staging waits for it (same stream: stream order)
     if (!direct && !capturing && h->work_used && h->work_stream != s) HIP_TRY(hipStreamWaitEvent(s, h->work_ev, 0));
@@ -714,7 +717,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         // no X at all: chain is +0; X^T stays zero
         HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
     } else if ((h->kind != tsg_tcsc::kJit ? tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s)
-                : r64                      ? tsg::launch_transpose_quads(dX, h->d_work, M, K, Mp, Kp, s)
+                : r64                      ? tsg::launch_transpose_quads(dX, h->d_work, M, K, Mp, Kp, jv->piece_rows, s)
                                            : tsg::launch_transpose_pairs(dX, h->d_work, M, K, Mp, Kp, s)) != 0) {
         return fail(TSG_ERR_HIP, std::string("transpose launch: ") + hipGetErrorString(hipGetLastError()));
     }

@@ -125,6 +125,13 @@ constexpr uint32_t kJitFarFlag = 1u << 17;
 constexpr int kJit64TileM = 64;
 constexpr int kJit64Chunk = 192;
 constexpr uint32_t kJit64Format = 3;                    // region header word 7 bits 8-15: blocked k-quad layout
+// region header word 7 bit 18 (64-row image): pieces of 16 rows x 4 quads
+// (row base (r / 16) KiB + (r % 16) * 16: every ds_read_b128 lane group on 16
+// distinct 16-B slots, no bank conflict; direct-X pieces read 64 B of each
+// row) instead of 8 rows x 8 quads (whole 128-B lines per row; 2-way bank
+// conflicts on ds_read_b128).  TSG_JIT_QBLOCK=16|8 picks (A/B).
+constexpr uint32_t kJit64R16Flag = 1u << 18;
+int jit64_piece_rows();  // 16 (default) or 8 (TSG_JIT_QBLOCK=8); tsg_jit.cpp
 
 // Stream width: columns per generated stream.  kJitNW (64) is the default;
 // narrower streams (32, 16, 8: same register contract, fewer accumulators,
@@ -143,6 +150,7 @@ constexpr int kJitTailPadWords = 32768 + 1024;
 struct JitImage {
     int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0, waves = kJitWaves;
     int tile_m = kJitTileM, chunk = kJitChunk;  // 64 / kJit64Chunk for the 64-row image
+    int piece_rows = 0;                          // 64-row image: rows per DMA piece (16 or 8)
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
     std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
 };
@@ -223,8 +231,9 @@ int encode_fill(const int32_t *dW, int K, int N, const int32_t *d_csp, const int
 int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, void *stream);
 // X [M][K] -> X^T in the k-pair layout of the jit kernel (Kp even, Mp even)
 int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int Kp, void *stream);
-// X [M][K] -> the blocked k-quad layout of the 64-row image (Mp % 64 == 0, Kp % 192 == 0)
-int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, void *stream);
+// X [M][K] -> the blocked k-quad layout of the 64-row image (Mp % 64 == 0, Kp % 192 == 0;
+// piece_rows 16 or 8, kJit64R16Flag)
+int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream);
 int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                    const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                    int prelu, void *stream);

@@ -235,6 +235,12 @@ std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw, int C = k
 
 }  // namespace
 
+int jit64_piece_rows()
+{
+    const char *v = knob_value("TSG_JIT_QBLOCK");
+    return v && v[0] == '8' ? 8 : 16;
+}
+
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
                     int K, int N, int B, JitImage &img, int nw, int waves, bool far, bool r64)
 {
@@ -245,6 +251,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // K rows per chunk and per LDS unit (a pair, or a quad in the 64-row image):
     // 48 units of 1 KiB per chunk either way
     const int CH = r64 ? kJit64Chunk : kJitChunk, U = r64 ? 4 : 2;
+    // 64-row image: rows per DMA piece PR (16 or 8) and quads per piece 64 / PR
+    // (tsg_internal.h, kJit64R16Flag)
+    const int PR = r64 ? jit64_piece_rows() : 0, PQ = r64 ? 64 / PR : 0;
     const JitRegs R(waves);
     const int streams = waves;  // one stream per wave (no M split)
     const int kPieces = R.pieces;
@@ -257,6 +266,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     img.waves = waves;
     img.tile_m = r64 ? kJit64TileM : kJitTileM;
     img.chunk = CH;
+    img.piece_rows = PR;
     img.Npad = ((N + tile_cols - 1) / tile_cols) * tile_cols;
     img.nch = std::max(1, (K + CH - 1) / CH);
     const int nch = img.nch, ntiles = img.Npad / tile_cols;
@@ -312,7 +322,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)kJitSlots | (uint32_t)img.tile_m << 16,
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
                              (uint32_t)kJitRing | (r64 ? kJit64Format : kJitFormat) << 8 |
-                                 (uint32_t)(m0k ? kJitM0kFlag : 0u) | (far ? kJitFarFlag : 0u)});
+                                 (uint32_t)(m0k ? kJitM0kFlag : 0u) | (far ? kJitFarFlag : 0u) |
+                                 (PR == 16 ? kJit64R16Flag : 0u)});
     const char *na = knob_value("TSG_JIT_NOALIGN");
     Emit E{code, !(na && na[0] == '1')};
     // TSG_JIT_CP="dma,touch": cache-policy bits of the LDS-DMA pieces and the
@@ -402,13 +413,13 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     int vm_step = 0;  // VMEM operations (DMA pieces, code touches) issued in the current step
     int cur_wave = 0;  // the wave whose stream is being generated
     auto dma_piece = [&](int q, int i) {
-        // 64-row image: piece pr holds quads 8 (pr / 8) .. + 7 of the chunk
-        // (tsg_internal.h, blocked k-quad layout); pieces whose quads all lie
-        // at or past K are never staged (no entry reads them): the dispatcher
-        // may then stage straight from row-major X, whose rows end at K
-        // (tsg_jit_kernel.hip "direct X", K % 32 == 0).  They are a suffix of
-        // the wave's pieces, so no M0 group loses its first piece.
-        if (r64 && 32 * ((int64_t)plan[(size_t)q].chunk * (CH / 32) + ((int64_t)cur_wave * kPieces + i) / 8) >= K)
+        // 64-row image: piece pr holds quads PQ * (pr / (64 / PR)) .. + PQ - 1
+        // of the chunk (tsg_internal.h, blocked k-quad layout); pieces whose
+        // quads all lie at or past K are never staged (no entry reads them):
+        // the dispatcher may then stage straight from row-major X, whose rows
+        // end at K (tsg_jit_kernel.hip "direct X", K % (4 PQ) == 0).  They are
+        // a suffix of the wave's pieces, so no M0 group loses its first piece.
+        if (r64 && (int64_t)plan[(size_t)q].chunk * CH + 4 * PQ * (((int64_t)cur_wave * kPieces + i) / (64 / PR)) >= K)
             return;
         const uint32_t sub = m0k ? (uint32_t)(i & 3) : 0u;
         if (sub == 0) {
@@ -486,8 +497,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     const uint32_t dst = kXSlot0 + (uint32_t)(kJitSlotRegs * (issued % S));
                     const uint32_t lb = kLdsBaseV + (uint32_t)(rq % kJitRing);
                     // 64-row image, blocked k-quad layout: quad q of the chunk at
-                    // (q / 8) * 8 KiB + (q % 8) * 128 B from the lane's base
-                    const uint32_t off = r64 ? (uint32_t)(rd.pair / 8) * 8192u + (uint32_t)(rd.pair % 8) * 128u
+                    // (q / PQ) * 64 KiB / PR + (q % PQ) * 16 PR B from the lane's base
+                    const uint32_t off = r64 ? (uint32_t)(rd.pair / PQ) * (65536u / (uint32_t)PR) +
+                                                   (uint32_t)(rd.pair % PQ) * 16u * (uint32_t)PR
                                              : (uint32_t)rd.pair * kPairBytes;
                     if (r64) {
                         const QuadRead qr = quad_read(rd.mask);

@@ -81,6 +81,7 @@ static_assert(kJBufBytes == kJUnits * 1024, "one LDS-DMA piece per unit row");
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
 constexpr uint32_t kJM0kFlag = 1u << 16;  // header word 7: piece offsets in the DMA instruction (tsg_internal.h)
 constexpr uint32_t kJFormat = kJRows64 ? 3u : 2u;  // header word 7 bits 8-15: the X^T layout the code expects
+constexpr uint32_t kJR16Flag = 1u << 18;            // header word 7: 64-row image pieces of 16 rows x 4 quads
 #if TSG_JIT_ROWS64
 #define TSG_JIT_KERNEL_NAME tsg_jit64_kernel
 #else
@@ -176,8 +177,11 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
     const int ncol0 = nt * kJTileCols + stream * kJNW;
     const uint64_t cp = base + __builtin_amdgcn_readfirstlane(wcode[(size_t)nt * kJWaves + stream]);
     // the lane's LDS base in ring buffer 0 (64-row image, blocked k-quad
-    // layout: row r at (r / 8) KiB + (r % 8) * 16; tsg_internal.h)
-    const uint32_t lb0 = kJRows64 ? (uint32_t)(lane >> 3) * 1024u + (uint32_t)(lane & 7) * 16u : (uint32_t)lane * 16u;
+    // layout, PR rows per piece: row r at (r / PR) KiB + (r % PR) * 16;
+    // tsg_internal.h)
+    const uint32_t pr_rows = (hdr[7] & kJR16Flag) ? 16u : 8u;
+    const uint32_t lb0 = kJRows64 ? ((uint32_t)lane / pr_rows) * 1024u + ((uint32_t)lane % pr_rows) * 16u
+                                  : (uint32_t)lane * 16u;
     const uint32_t lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
     // LDS-DMA piece i of this wave = pair row pr = wave * P + i of the chunk: the
     // lane's 16 B at ((pr * Mp/2) + m0/2 + lane) * 16 from the chunk base (64-row
@@ -187,14 +191,15 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
     // here (never negative: pr >= i and a pair row of X^T is >= 1 KiB)
     const uint32_t m0k = (hdr[7] & kJM0kFlag) ? 1u : 0u;
     uint32_t off[kJPieces];
-    // 64-row image (blocked k-quad layout, tsg_internal.h): piece pr = 8 qg +
-    // rg, DMA lane j carries row 8 rg + j % 8, quad 8 qg + j / 8.  Staged:
+    // 64-row image (blocked k-quad layout, tsg_internal.h): piece pr = (64 /
+    // PR) qg + rg, DMA lane j carries row PR rg + j % PR, quad (64 / PR) qg + j
+    // / PR.  Staged:
     // the piece is the 1 KiB at ((chunk * Mt + mt) * 48 + pr) KiB of the
     // staged copy.  Direct X (xrow > 0 floats per row): the quad X[m][4q ..
     // 4q+3] is 16 contiguous bytes of row-major X, so the pieces stage straight
     // from X -- no X^T pass; rows past M read row M-1 (their results are never
     // stored), pieces at or past K are never staged (the generated code omits
-    // them; K % 32 == 0), and the chunk base starts 3 KiB below X so that
+    // them; K % (256 / PR) == 0), and the chunk base starts 3 KiB below X so that
     // off[i] stays non-negative after the m0k subtraction.
     const bool direct = kJRows64 && xrow > 0;
     const uint32_t xrow_b = (uint32_t)xrow * 4u;
@@ -205,8 +210,9 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
         if (!kJRows64) {
             o = (pr * ((uint32_t)Mp / 2u) + (uint32_t)m0 / 2u + (uint32_t)lane) * 16u;
         } else if (direct) {
-            const uint32_t row = (uint32_t)min(m0 + (int)(pr & 7u) * 8 + (lane & 7), M - 1);
-            o = row * xrow_b + ((pr >> 3) * 8u + (uint32_t)(lane >> 3)) * 16u + 3072u;
+            const uint32_t rgs = 64u / pr_rows;  // row groups per tile = quads per piece
+            const uint32_t row = (uint32_t)min(m0 + (int)((pr % rgs) * pr_rows + (uint32_t)lane % pr_rows), M - 1);
+            o = row * xrow_b + ((pr / rgs) * rgs + (uint32_t)lane / pr_rows) * 16u + 3072u;
         } else {
             o = ((uint32_t)mt * (uint32_t)kJUnits + pr) * 1024u + (uint32_t)lane * 16u;
         }

@@ -38,11 +38,13 @@ class Geom:
         # format 3: the 64-row image -- k-quad X^T, 64-row tiles, VOP2 adds
         assert fmt in (2, 3), "region must use the k-pair (2) or k-quad (3) X^T layout"
         self.r64 = fmt == 3
+        # 64-row image: rows per DMA piece (bit 18: 16 rows x 4 quads, else 8 x 8)
+        self.pr_rows = (16 if (int(code[7]) >> 18) & 1 else 8) if self.r64 else 0
         assert self.streams == self.waves and self.msplit == 1 and self.tile_m == (64 if self.r64 else 128)
         # DMA pieces take their in-group offset from the instruction offset (one
         # M0 per 4 pieces; the dispatcher subtracts it from the global offsets)
         self.m0k = (int(code[7]) >> 16) & 1
-        assert int(code[7]) >> 18 == 0  # bit 16: m0k, bit 17: far-X^T image
+        assert int(code[7]) >> 19 == 0 and (self.r64 or (int(code[7]) >> 18) & 1 == 0)  # 16 m0k, 17 far, 18 R16
         self.unit = 4 if self.r64 else 2              # k rows per LDS unit (quad / pair)
         self.pairs = self.chunk // self.unit          # units per chunk
         self.pair_bytes = self.tile_m * 4 * self.unit  # one unit row of the tile in LDS: 1 KiB
@@ -213,11 +215,13 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     assert rem == 0 and 0 <= j < nch
                     dst = wv.m0 + off  # the offset applies to the LDS address too
                     assert dst % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
-                    if G.r64:  # blocked k-quad piece pr = 8 qg + rg: lane slot l = row 8 rg + l % 8, quad 8 qg + l / 8
-                        qg, rg = divmod(pr, 8)
+                    if G.r64:  # blocked k-quad piece pr = Q qg + rg: lane slot l = row R rg + l % R, quad Q qg + l / R
+                        R = G.pr_rows
+                        Q = 64 // R
+                        qg, rg = divmod(pr, Q)
                         lanes = np.arange(64)
-                        q = j * PAIRS + 8 * qg + lanes // 8
-                        data = XP[q, m0 + 8 * rg + lanes % 8].reshape(-1).copy()
+                        q = j * PAIRS + Q * qg + lanes // R
+                        data = XP[q, m0 + R * rg + lanes % R].reshape(-1).copy()
                     else:
                         data = XP[j * PAIRS + pr, m0 // RPL:m0 // RPL + 64].reshape(-1).copy()
                     wv.pending.append([(dst, data, phase)])
@@ -243,13 +247,15 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     buf = a - G.lds_v
                     if G.r64:
                         # blocked k-quad layout: lane l's base (dispatcher) = buffer +
-                        # (l / 8) KiB + (l % 8) * 16; quad q at (q / 8) * 8 KiB + (q % 8) * 128
-                        sub = off % 128
-                        assert sub in allowed and off // 8192 < PAIRS // 8
+                        # (l / R) KiB + (l % R) * 16; quad q at (q / Q) * 64 KiB / R + (q % Q) * 16 R
+                        R = G.pr_rows
+                        Q = 64 // R
+                        sub = off % (16 * R)
+                        assert sub in allowed and off // (65536 // R) < PAIRS // Q
                         lanes = np.arange(64)
-                        addr = buf * BUF_BYTES + (lanes // 8) * 1024 + (lanes % 8) * 16 + off
+                        addr = buf * BUF_BYTES + (lanes // R) * 1024 + (lanes % R) * 16 + off
                         pieces = np.unique(addr // PAIR_BYTES)
-                        assert len(pieces) == 8 and all(0 <= landed[p] < phase for p in pieces), \
+                        assert len(pieces) == Q and all(0 <= landed[p] < phase for p in pieces), \
                             "LDS read of data not yet landed before a barrier"
                         for p in pieces:
                             last_read[p] = max(last_read[p], phase)
