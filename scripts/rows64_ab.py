@@ -59,7 +59,7 @@ for M in (int(v) for v in a.M.split(",")):
     X = (torch.randint(-(1 << 23), 1 << 23, (M, a.K), generator=g, device="cuda", dtype=torch.int32).float()
          * torch.exp2(-torch.randint(0, 24, (M, a.K), generator=g, device="cuda").float()))
     out = {"M": M, "K": a.K, "N": a.N, "s": a.s, "waves_env": os.environ.get("TSG_JIT_WAVES"),
-           "xdirect_env": os.environ.get("TSG_JIT_XDIRECT")}
+           "xdirect_env": os.environ.get("TSG_JIT_XDIRECT"), "qblock_env": os.environ.get("TSG_JIT_QBLOCK")}
     ref = None
     for mode in a.modes.split(","):
         for w in ([0] if mode == "ell" else [int(x) for x in a.widths.split(",")]):
