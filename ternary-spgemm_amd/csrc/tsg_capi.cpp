@@ -107,13 +107,16 @@ namespace {
 // pick_ell_variant), the variant with 8-row tiles, and the M up to which
 // 8-row tiles are used.
 constexpr int kEllAutoMaxM = 32;
-constexpr int kEllAutoMaxMChunked = 32;
+constexpr int kEllAutoMaxMChunked = 16;
 constexpr int kEllTile8 = 2;
 constexpr int kEllMidM = 32;
 constexpr int64_t kEllPcRowsMaxMN = 32768;
 constexpr int kEllStarvedMaxM = 1024;
-// Largest M the automatic choice sends to the 64-row image (pick_rows64)
+// M up to which the automatic choice always takes the 64-row image, and the
+// filled fraction of its last round below which the 128-row image's widest
+// shape loses to it (pick_rows64)
 constexpr int kRows64AutoMaxM = 512;
+constexpr double kRows64FullRound = 0.9;
 constexpr int64_t kJitFullWgs = 230;
 constexpr int64_t kJitOneRoundWgs = 256;  // one jit workgroup per CU (144 KiB of LDS)
 constexpr double kFarXtBytes = 768.0 * 1024 * 1024;  // X^T >= 3x the 256 MiB Infinity Cache
@@ -275,45 +278,62 @@ bool far_xt(const tsg_tcsc *h, int M)
     return long_map && 4.0 * (double)M * (double)h->K >= kFarXtBytes && 8.0 * nnz <= kFarCodeBytes;
 }
 
-// The 64-row image stages its pieces straight from row-major X (PR rows x
+// The 64-row image can stage its pieces straight from row-major X (PR rows x
 // 1024 / PR contiguous bytes each; tsg_internal.h) when rows start 16-B
 // aligned (X 16-B aligned, K % 4 == 0), no piece straddles K (K % (256 / PR)
 // == 0: pieces at or past K are omitted, so nothing reads past a row's end)
-// and the per-lane
-// offsets fit 32 bits; TSG_JIT_XDIRECT=0 forces the staged copy (A/B).
+// and the per-lane offsets fit 32 bits -- on request only (TSG_JIT_XDIRECT=1,
+// read per call): every workgroup of an M tile gathers the same rows, 4K
+// bytes apart, chunk after chunk, and the kernel loses more than the X^T pass
+// costs at every M measured (profiles/r04f_shape_ab.jsonl,
+// r04g_bound_ab.jsonl; kernel / step us, K = 4096, N = 16384: M = 64
+// 85.2-85.7 / 91.6-92.4 direct vs 65.5-65.9 / 78.9-79.5 staged, either piece
+// shape; M = 512 208-209 / 215 vs 202-205 / 217-220; N = 4096: M = 256
+// 81.3 / 87.7 vs 56.7 / 71.1, M = 512 100.8 / 107.0-107.3 vs 92.0-92.6 /
+// 107.5-108.3).
 bool x_direct(const float *dX, int M, int K, int piece_rows)
 {
-    static const bool on = [] {
-        const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
-        return !(e && e[0] == '0');
-    }();
+    const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
+    const bool on = e && e[0] == '1';
     return on && K > 0 && piece_rows > 0 && K % (256 / piece_rows) == 0 && ((uintptr_t)dX & 15) == 0 &&
            (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
 }
 
+JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64 = false);
+
 // The 64-row image (VOP2 adds, one M row per lane) or the 128-row one
 // (v_pk_add_f32, two rows per lane) for a call with M rows (that the small-M
 // walk does not take); BlockedTCSC runs the 128-row image only.  Measured
-// (profiles/r04d_rows64_ab.jsonl, r04d_rows64_big.jsonl; kernel / step us,
-// same box): at K = 4096, N = 16384 the 64-row image wins from M = 48 (68 vs
-// ELL 95 / 128-row 107) through M = 512 (202 / 209 vs 228 / 243; M = 64 78 /
-// 84 vs 108 / 121, M = 128 90 / 96 vs 110 / 123, M = 256 119 / 125 vs 150 /
-// 164), and configs[1] (512, 4096, 4096) by its step (107 vs 112: no X^T
-// pass); from M = 1024 the 128-row image is as fast or faster (configs[2]
-// 1314 / 1351 vs 1405 / 1411).  tcsc_hip_set_tile_rows pins one;
-// TSG_JIT_ROWS64_MAXM moves the boundary (A/B).
+// (profiles/r04f_shape_ab.jsonl, r04g_bound_ab.jsonl, r04h_big_ab.jsonl; step
+// us, X staged for both): the 64-row image wins at every M <= 512 (K = 4096,
+// N = 16384: M = 64 79 vs 121, M = 192 130 vs 163, M = 512 217 vs 243;
+// configs[1] 108 vs 116) and above that wherever the 128-row image's shape is
+// narrower than 64 x 8 or leaves a round partly empty (N = 16384: M = 640 336
+// vs 385, M = 1536 547 vs 617; N = 8192, M = 1024 204 vs 236; N = 4096, M =
+// 2048 224 vs 245; K = 16384, N = 4096, M = 2048 806 vs 973); the 128-row
+// image keeps the calls its widest shape fills in whole rounds (configs[2]
+// 1360 vs 1437, N = 16384 M = 1024 339 vs 358, N = 8192 M = 4096 686 vs 708,
+// s = 8 / 16 862 / 637 vs 880 / 661).  tcsc_hip_set_tile_rows pins one;
+// TSG_JIT_ROWS64_MAXM replaces the rule by M <= its value (A/B).
 bool pick_rows64(const tsg_tcsc *h, int M)
 {
-    static const int max_m = [] {
+    static const int env_max = [] {
         const char *e = tsg::knob_value("TSG_JIT_ROWS64_MAXM");
-        return e ? atoi(e) : kRows64AutoMaxM;
+        return e ? atoi(e) : -1;
     }();
     if (h->B || h->kind != tsg_tcsc::kJit) return false;
     if (h->tile_rows) return h->tile_rows == 64;
-    return M <= max_m;
+    if (env_max >= 0) return M <= env_max;
+    if (M <= kRows64AutoMaxM) return true;
+    const JitShape s = pick_jit_shape(h, M, false);
+    if (s.nw != tsg::kJitNW || s.waves != tsg::kJitWaves) return true;
+    const int64_t wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
+                        ((h->N + (int64_t)s.waves * s.nw - 1) / ((int64_t)s.waves * s.nw));
+    const int64_t rounds = (wgs + kJitOneRoundWgs - 1) / kJitOneRoundWgs;
+    return (double)wgs < kRows64FullRound * (double)(rounds * kJitOneRoundWgs);
 }
 
-JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64 = false)
+JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
 {
     static const int env_waves = [] {
         const char *e = tsg::knob_value("TSG_JIT_WAVES");
@@ -553,15 +573,17 @@ bool use_ell_pc(const tsg_tcsc *h, int v) { return v == 0 && ell_pc_available(h)
 // kernel cannot fill the GPU; -1 = the jit (or rx) kernel.  Measured on
 // configs[2]'s and configs[0]'s K, N (profiles/r02u_ell_lg.txt): up to M = 8
 // the smallest M tile that holds M; up to M = 32 tiles of 8 (2 rows per lane:
-// an 8-row chunk of K = 4096 fits LDS, one stream per column); above that the
-// largest tile whose chunk holds K.  Automatic up to M = 32 (round 4: the
-// 64-row image takes 32 < M, K = 4096, N = 16384: M = 32 ELL 51 / step 58 vs
-// 59 / 65 us, M = 48 95 vs 68 us, M = 64 97 vs 78 us; K = N = 16384 M = 32
-// 0.29 vs 0.39 ms on the 128-row image, profiles/r03_half_tile_ab.txt); and up to M = 1024 while the
-// jit kernel would have at most 64 workgroups (the reference's (1000, 2048,
-// 512): 31 vs 52 us; (256, 4096, 1024): 34 vs 91 us; at 128 workgroups the
-// jit kernel wins: (1024, 1024, 1024) 32 vs 35 us;
-// profiles/r02_ell_vs_jit_ref.jsonl).
+// an 8-row chunk of K <= 5116 fits LDS, one stream per column); above that the
+// largest tile whose chunk holds K.  Automatic (round 4, against the 64-row
+// image, profiles/r04g_bound_ab.jsonl, step us) up to M = 32 while an 8-row
+// chunk holds K (K = 4096, N = 16384: M = 32 56 vs 70, M = 48 101 vs 71), up to
+// M = 16 when K is chunked (K = N = 16384: M = 16 184 vs 247, M = 32 310 vs
+// 248; K = 16384, N = 4096: M = 16 178 vs 158, M = 32 281 vs 155); and, while
+// an 8-row chunk holds K, up to M = 1024 when the jit kernel would have at
+// most 64 workgroups (the reference's (1000, 2048, 512): 38 vs 52 us;
+// (256, 4096, 1024): 41 vs 82; (256, 2048, 2048): 37 vs 47; at 128 workgroups
+// the jit kernel wins: (1024, 1024, 1024) 43 vs 35).  With K chunked the
+// starved grid goes to the 64-row image ((64, 16384, 4096): 266 vs 156 us).
 int pick_ell_variant(const tsg_tcsc *h, int M)
 {
     if (h->kind != tsg_tcsc::kJit || h->B || h->small_m == 1) return -1;
@@ -569,7 +591,7 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // the jit kernel's workgroups at its narrowest width (8 columns per wave)
     const int64_t jit_wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                             ((h->N + 8 * tsg::kJitWaves - 1) / (8 * tsg::kJitWaves));
-    const bool starved = M <= kEllStarvedMaxM && jit_wgs <= kEllStarvedWgs;
+    const bool starved = one8 && M <= kEllStarvedMaxM && jit_wgs <= kEllStarvedWgs;
     static const int auto_max = [] {  // TSG_ELL_MAXM: A/B of the small-M boundary
         const char *e = tsg::knob_value("TSG_ELL_MAXM");
         return e ? atoi(e) : kEllAutoMaxM;

@@ -32,7 +32,14 @@ import pytest
     ((64, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=4, far=False, map=(4, 1), tmask=0)),
     # M = 192: one round of 32 x 8 (192 workgroups), not 1.5 rounds of 32 x 4 (178 us measured)
     ((192, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(4, 3), tmask=0)),
-    ((1024, 4096, 1024, 4), dict(kernel="tsg_jit_kernel", width=8, waves=4, far=False, map=(4, 8), tmask=3)),
+    # above M = 512 the 64-row image wherever the 128-row image's shape is narrower than
+    # 64 x 8 or leaves a round partly empty (r04h_big_ab.jsonl, step us): M = 640 336 vs 385,
+    # N = 4096 M = 1024 147 vs 160 (and (1024, 4096, 1024), r04i_plan_ab.jsonl) ...
+    ((640, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(2, 10), tmask=0)),
+    ((1024, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(2, 16), tmask=3)),
+    ((1024, 4096, 1024, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=4, far=False, map=(2, 16), tmask=3)),
+    # ... the 128-row image where 64 x 8 fills whole rounds: M = 1024 339 vs 358
+    ((1024, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=3)),
 ])
 def test_plan_matches_measured_winners(tsg, shape, plan):
     M, K, N, s = shape
@@ -48,11 +55,15 @@ def test_plan_matches_measured_winners(tsg, shape, plan):
     (64, 4096, 16384, "tsg_jit64_kernel"),
     (96, 4096, 16384, "tsg_jit64_kernel"),
     (512, 4096, 16384, "tsg_jit64_kernel"),
-    (513, 4096, 16384, "tsg_jit_kernel"),         # the 128-row image from M > 512 (configs[2]: 1314 vs 1405 us)
+    (1536, 4096, 16384, "tsg_jit64_kernel"),      # 128-row 64 x 8 in 1.5 rounds (547 vs 617 us, r04h)
+    (2048, 4096, 16384, "tsg_jit_kernel"),        # ... in whole rounds (695 vs 697 us; configs[2] 1360 vs 1437)
     (32, 1024, 4096, "tsg_tcsc_ell_kernel"),      # configs[0]
-    (32, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 32
+    (16, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 16 (184 vs 247 us, r04g)
+    (17, 16384, 16384, "tsg_jit64_kernel"),       # (M = 32: 310 vs 248 us)
     (40, 16384, 16384, "tsg_jit64_kernel"),
-    (1000, 2048, 512, "tsg_tcsc_ell_kernel"),     # starved jit grid (<= 64 workgroups)
+    (1000, 2048, 512, "tsg_tcsc_ell_kernel"),     # starved jit grid (<= 64 workgroups), K in one chunk
+    (256, 4096, 1024, "tsg_tcsc_ell_kernel"),     # (41 vs 82 us, r04g)
+    (64, 16384, 4096, "tsg_jit64_kernel"),        # starved but K chunked: 156 vs 266 us (r04g)
 ])
 def test_plan_small_m_kernel(tsg, M, K, N, kernel):
     assert tsg.call_plan(K, N, K * N // 4, M)["kernel"] == kernel

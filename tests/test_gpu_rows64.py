@@ -132,14 +132,16 @@ def test_rows64_full_y_configs2_kn(tsg, oracle_mod, M):
 @pytest.mark.parametrize("M,K", [(1, 1024), (64, 4096), (130, 1000), (37, 192 * 3), (70, 208), (70, 196)])
 def test_rows64_direct_x_and_staged(tsg, oracle_mod, monkeypatch, M, K, qblock):
     """The 64-row image stages its DMA pieces straight from row-major X when
-    the rows are 16-B aligned and no piece straddles K (tsg_jit_kernel.hip
-    "direct X": no X^T pass), and through the blocked staged copy otherwise:
-    X at a 4-byte offset takes the staged path.  Both piece shapes of the
+    asked to (TSG_JIT_XDIRECT=1; automatic above one 64-row tile), the rows
+    are 16-B aligned and no piece straddles K (tsg_jit_kernel.hip "direct X":
+    no X^T pass), and through the blocked staged copy otherwise: X at a
+    4-byte offset takes the staged path.  Both piece shapes of the
     blocked layout (TSG_JIT_QBLOCK: 16 rows x 4 quads, 8 x 8).  Bit-exact
     against the oracle (rows past M read row M-1 and are dropped; pieces past
     K are never staged)."""
     import torch
     monkeypatch.setenv("TSG_JIT_QBLOCK", qblock)
+    monkeypatch.setenv("TSG_JIT_XDIRECT", "1")
     O = oracle_mod
     N = 333
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, M + K))

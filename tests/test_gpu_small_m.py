@@ -157,11 +157,14 @@ def test_config0_runs_small_m(tsg, oracle_mod):
 
 
 @pytest.mark.parametrize("M,K,N,small", [(512, 2048, 512, True), (1000, 2048, 512, True), (256, 4096, 1024, True),
-                                         (128, 9000, 1024, True), (1024, 1024, 1024, False), (96, 4096, 16384, False)])
+                                         (128, 9000, 1024, False), (1024, 1024, 1024, False), (96, 4096, 16384, False),
+                                         (64, 16384, 4096, False)])
 def test_starved_jit_shapes_take_small_m(tsg, oracle_mod, M, K, N, small):
     """The reference's cases where the jit kernel would have <= 64 workgroups
     (plots/run_benchmark.py:8-33) take the small-M kernel automatically up to
-    M = 1024; bit for bit on sampled rows either way."""
+    M = 1024 while an 8-row chunk holds K (K <= 5116; with K chunked the
+    64-row image: (64, 16384, 4096) 156 vs 266 us, profiles/r04g_bound_ab.jsonl);
+    bit for bit on sampled rows either way."""
     import torch
     O = oracle_mod
     arrs = tsg.gen_tcsc(K, N, 4, 7)
