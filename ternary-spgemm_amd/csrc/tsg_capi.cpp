@@ -351,11 +351,15 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
         // 64-row image: the shape with the least modelled time = rounds of
         // one-workgroup-per-CU x the time of a workgroup, which grows with the
         // columns a SIMD carries (width x waves / 4) scaled by density, over a
-        // fixed part (the K sweep's staging and barriers).  Fitted on one
-        // full round at K = 4096, s = 4 (profiles/r04d_rows64_ab.jsonl): 16 x 4
-        // 78 us, 32 x 4 93, 16 x 8 91, 32 x 8 110-118, 64 x 8 202 us ~ 1.15 x
-        // (48 + columns per SIMD).  A fractional round costs a whole one (M =
-        // 192: 32 x 4 on 384 workgroups 178 us; one round of 32 x 8 ~ 115).
+        // fixed part (the K sweep's staging and barriers).  A lone wave per
+        // SIMD (4-wave workgroups) issues its VOP2 adds at half the rate of a
+        // pair, and 8-column streams feed few adds per X read.  Fitted on
+        // one-round grids at K = 4096, s = 4 with X staged
+        // (profiles/r04j_waves_ab.jsonl, kernel us): configs[1] 16 x 8 79.6 vs
+        // 32 x 4 92.8; M = 128, N = 16384: 16 x 8 87.1 vs 32 x 4 91.3-96.7;
+        // M = 64: 16 x 4 66.2 vs 8 x 8 76.0; M = 256, N = 4096: 16 x 4
+        // 56.1-58.9 vs 8 x 8 59.3.  A fractional round costs a whole one
+        // (M = 192: 32 x 4 on 384 workgroups 178 us; one round of 32 x 8 123).
         // Ties go to the wider stream (fewer LDS reads per add).
         const double dens4 = 4.0 * (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
         JitShape pick{tsg::kJitNW, tsg::kJitWaves, false, true};
@@ -369,7 +373,8 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
                 const double image = image8 + (double)ntile * waves * h->jit_nch * 2 * (160.0 + 8.0 * tsg::kJitChunk);
                 if (nw != tsg::kJitNW && image > 2.0 * (double)(1ull << 30)) continue;
                 const double rounds = (double)((wgs + kJitOneRoundWgs - 1) / kJitOneRoundWgs);
-                const double cost = rounds * (48.0 + (double)nw * waves / 4.0 * dens4);
+                const double adds = (double)nw * waves / 4.0 * dens4 * (waves == 4 ? 1.35 : 1.0);
+                const double cost = rounds * (48.0 + adds + (nw == 8 ? 10.0 : 0.0));
                 if (!any || cost < best_cost) {
                     any = true;
                     best_cost = cost;

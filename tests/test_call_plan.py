@@ -9,9 +9,10 @@ import pytest
 @pytest.mark.parametrize("shape,plan", [
     # configs[2] (the bench): 64 x 8, CU pairs on one code stream (2 x 16)
     ((4096, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(2, 16), tmask=0)),
-    # configs[1]: the 64-row image, 32 x 4 one-round grid, code touches thinned (round 4:
-    # step 107 vs 112 us for the 128-row image's 16 x 4, r04d_rows64_big.jsonl)
-    ((512, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=4, far=False, map=(4, 8), tmask=3)),
+    # configs[1]: the 64-row image, 16 x 8 one-round grid (two waves per SIMD), code touches
+    # thinned (round 4, r04j_waves_ab.jsonl: kernel / step 79.6 / 95.5 us vs 32 x 4 92.8 / 108.4;
+    # the 128-row image's 16 x 4 96.8-100.3 / 111.8-115.9, r04g)
+    ((512, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(4, 8), tmask=3)),
     # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt)
     ((4096, 4096, 16384, 16), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=0)),
     # the reference's largest case: s = 4 far-X^T image on 1 x 32 (r03e_far_ab.txt) ...
@@ -28,7 +29,7 @@ import pytest
     # the shape of least modelled time (tsg_capi.cpp pick_jit_shape)
     ((256, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(4, 4), tmask=3)),
     ((512, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=3)),
-    ((128, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=4, far=False, map=(4, 2), tmask=0)),
+    ((128, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(4, 2), tmask=0)),  # 87.1 vs 32 x 4 91-97 us
     ((64, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=4, far=False, map=(4, 1), tmask=0)),
     # M = 192: one round of 32 x 8 (192 workgroups), not 1.5 rounds of 32 x 4 (178 us measured)
     ((192, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(4, 3), tmask=0)),
