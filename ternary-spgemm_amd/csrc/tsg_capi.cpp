@@ -53,7 +53,7 @@ struct tsg_tcsc {
         int64_t code_bytes = 0, wcode_words = 0;
     };
     JitVariant jv[8];                     // 7: the 64 x 8 "far X^T" image (pick_jit_shape)
-    JitVariant jv64[7];                   // the 64-row image (tsg_internal.h), shape_index 0..6
+    JitVariant jv64[8];                   // the 64-row image (tsg_internal.h), shape_index 0..7
     int jit_nch = 0;                      // X^T chunks (all widths)
     int jit64_nch = 0;                    // X^T chunks of the 64-row image (192 rows each)
     int tile_rows = 0;                    // tcsc_hip_set_tile_rows: 0 auto, 128 or 64 (jit images)
@@ -220,9 +220,11 @@ int width_index(int nw)
 }
 
 // jv index of a (width, waves) shape: 8-wave widths 0..3, 4-wave widths
-// 32/16/8 4..6, the 64 x 8 far-X^T image 7
+// 32/16/8 4..6, the 64 x 8 far-X^T image 7; jv64 (the 64-row image): the
+// same 0..6 and 128 x 8 at 7
 int shape_index(int nw, int waves, bool far = false)
 {
+    if (nw == tsg::kJit64WideNW) return waves == tsg::kJitWaves && !far ? 7 : -1;
     const int w = width_index(nw);
     if (w < 0 || !tsg::jit_waves_ok(nw, waves) || (far && (nw != tsg::kJitNW || waves != tsg::kJitWaves))) return -1;
     return far ? 7 : waves == tsg::kJitWaves ? w : 3 + w;
@@ -323,6 +325,7 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     }();
     if (h->B || h->kind != tsg_tcsc::kJit) return false;
     if (h->tile_rows) return h->tile_rows == 64;
+    if (h->jit_force == tsg::kJit64WideNW) return true;  // only the 64-row image has that width
     if (env_max >= 0) return M <= env_max;
     if (M <= kRows64AutoMaxM) return true;
     const JitShape s = pick_jit_shape(h, M, false);
@@ -341,8 +344,9 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
     }();
     if (h->B) return {tsg::kJitNW, tsg::kJitWaves};
     if (h->jit_force) {
-        const int w = env_waves == 4 && tsg::jit_waves_ok(h->jit_force, 4) ? 4 : tsg::kJitWaves;
-        return {h->jit_force, w, !r64 && h->jit_force == tsg::kJitNW && w == tsg::kJitWaves && far_xt(h, M), r64};
+        const int f = !r64 && h->jit_force == tsg::kJit64WideNW ? tsg::kJitNW : h->jit_force;
+        const int w = env_waves == 4 && tsg::jit_waves_ok(f, 4) ? 4 : tsg::kJitWaves;
+        return {f, w, !r64 && f == tsg::kJitNW && w == tsg::kJitWaves && far_xt(h, M), r64};
     }
     const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM;
     const int64_t mt = (std::max(M, 1) + tile_m - 1) / tile_m;
@@ -365,10 +369,11 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
         JitShape pick{tsg::kJitNW, tsg::kJitWaves, false, true};
         double best_cost = 0.0;
         bool any = false;
-        for (int nw : tsg::kJitWidths)
+        for (int nw : tsg::kJit64Widths)
             for (int waves : {tsg::kJitWaves, 4}) {
                 if (!tsg::jit_waves_ok(nw, waves)) continue;
-                if (env_waves == 4 && nw != tsg::kJitNW && waves != 4) continue;
+                if (nw == tsg::kJit64WideNW) continue;  // pinned only (tcsc_hip_set_jit_width) until measured
+                if (env_waves == 4 && nw < tsg::kJitNW && waves != 4) continue;
                 const int64_t ntile = (h->N + (int64_t)waves * nw - 1) / ((int64_t)waves * nw), wgs = mt * ntile;
                 const double image = image8 + (double)ntile * waves * h->jit_nch * 2 * (160.0 + 8.0 * tsg::kJitChunk);
                 if (nw != tsg::kJitNW && image > 2.0 * (double)(1ull << 30)) continue;
@@ -476,7 +481,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
                        bool r64 = false)
 {
     const int i = shape_index(nw, waves, far && !r64);
-    if (i < 0 || !tsg::jit_width_ok(nw) || (r64 && (far || h->B)))
+    if (i < 0 || !(r64 ? tsg::jit64_width_ok(nw) : tsg::jit_width_ok(nw)) || (r64 && (far || h->B)))
         return fail(TSG_ERR_ARG, "unsupported jit stream width " + std::to_string(nw) + " x " + std::to_string(waves) +
                                  " waves" + (r64 ? " (64-row image)" : ""));
     tsg_tcsc::JitVariant &v = r64 ? h->jv64[i] : h->jv[i];
@@ -1271,8 +1276,9 @@ extern "C" int tcsc_hip_set_jit_width(tsg_tcsc *h, int width)
 {
     if (!h) return fail(TSG_ERR_ARG, "null handle");
     if (h->kind != tsg_tcsc::kJit) return fail(TSG_ERR_ARG, "tcsc_hip_set_jit_width: not a jit handle");
-    if (width != 0 && (width_index(width) < 0 || !tsg::jit_width_ok(width) || (h->B && width != tsg::kJitNW)))
-        return fail(TSG_ERR_ARG, "tcsc_hip_set_jit_width: expected 0 (auto), 64, 32, 16 or 8 (64 for BlockedTCSC)");
+    if (width != 0 && (!tsg::jit64_width_ok(width) || (h->B && width != tsg::kJitNW)))
+        return fail(TSG_ERR_ARG, "tcsc_hip_set_jit_width: expected 0 (auto), 128 (64-row image), 64, 32, 16 or 8 "
+                                 "(64 for BlockedTCSC)");
     std::lock_guard<std::mutex> lk(h->mu);
     h->jit_force = width;
     return TSG_OK;

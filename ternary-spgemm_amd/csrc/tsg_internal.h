@@ -142,7 +142,13 @@ inline bool jit_width_ok(int nw) { return nw == kJitNW || nw == 32 || nw == 16 |
 // waves per workgroup: 8, or 4 for the narrow widths (lib/tsg_jit_w<nw>_4w.co):
 // the same 48 KiB chunks staged by 4 waves (12 DMA pieces each), half the
 // columns per workgroup -> twice the workgroups at mid M
-inline bool jit_waves_ok(int nw, int waves) { return waves == kJitWaves || (waves == 4 && nw != kJitNW); }
+inline bool jit_waves_ok(int nw, int waves) { return waves == kJitWaves || (waves == 4 && nw < kJitNW); }
+// The 64-row image also runs 128 columns per wave (8 waves; one accumulator
+// VGPR per column, v116..v243; lib/tsg_jit64_w128.co): twice the adds per
+// staged chunk and per X read of its 64-wide stream
+constexpr int kJit64WideNW = 128;
+constexpr int kJit64Widths[] = {kJit64WideNW, kJitNW, 32, 16, 8};
+inline bool jit64_width_ok(int nw) { return jit_width_ok(nw) || nw == kJit64WideNW; }
 
 // words of padding after the last stream (the code prefetch reads ahead)
 constexpr int kJitTailPadWords = 32768 + 1024;

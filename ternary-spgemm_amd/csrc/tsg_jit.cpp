@@ -160,6 +160,7 @@ struct JitRegs {
 };
 static_assert(((kDmaOffV + kJitChunk / 2 / kJitWaves + 2) & ~1u) + 2 * kJitNW <= 256u, "VGPR budget");
 static_assert(((kDmaOffV + kJitChunk / 2 / 4 + 2) & ~1u) + 2 * 32 <= 256u, "VGPR budget, 4 waves");
+static_assert(((kDmaOffV + kJitChunk / 2 / kJitWaves + 2) & ~1u) + kJit64WideNW <= 256u, "VGPR budget, 64-row x 128");
 // narrower streams (jit width < kJitNW) use the same register contract, fewer accumulators
 constexpr int kTailPad = kJitTailPadWords;  // words of padding after the last stream (code prefetch reads ahead)
 static_assert((kJitChunk / 2 - 1) * kPairBytes + 8 < 65536, "ds_read offset field");
@@ -247,6 +248,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     if (nw <= 0) nw = kJitNW;
     if (!jit_waves_ok(nw, waves)) waves = kJitWaves;
     if (B) r64 = false;  // BlockedTCSC: the 128-row image only
+    if (nw > kJitNW && !r64) nw = kJitNW;  // 128 columns per wave: the 64-row image only (callers check)
     if (r64) far = false;
     // K rows per chunk and per LDS unit (a pair, or a quad in the 64-row image):
     // 48 units of 1 KiB per chunk either way
@@ -797,9 +799,9 @@ extern "C" int tsg_jit_codegen64(const int32_t *csp, const int32_t *csn, const i
                                  int K, int N, int width, int waves, uint32_t *code, int64_t code_cap,
                                  int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
 {
-    if (!tsg::jit_width_ok(width) || !tsg::jit_waves_ok(width, waves)) {
+    if (!tsg::jit64_width_ok(width) || !tsg::jit_waves_ok(width, waves)) {
         g_tsg_host_err = "tsg_jit_codegen64: unsupported shape " + std::to_string(width) + " x " +
-                         std::to_string(waves) + " (widths 64, 32, 16, 8; 4 waves for the narrow ones)";
+                         std::to_string(waves) + " (widths 128, 64, 32, 16, 8; 4 waves for 32, 16, 8)";
         return TSG_ERR_ARG;
     }
     const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N, 0);

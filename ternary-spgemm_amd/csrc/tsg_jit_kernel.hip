@@ -66,9 +66,9 @@ namespace {
 #endif
 constexpr int kJWaves = TSG_JIT_WAVES;
 constexpr int kJNW = TSG_JIT_NW;
-static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8, "stream width");
-static_assert(kJWaves == 8 || (kJWaves == 4 && kJNW < 64), "waves per workgroup");
 constexpr bool kJRows64 = TSG_JIT_ROWS64 != 0;
+static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8 || (kJRows64 && kJNW == 128), "stream width");
+static_assert(kJWaves == 8 || (kJWaves == 4 && kJNW < 64), "waves per workgroup");
 constexpr int kJTileM = kJRows64 ? 64 : 128;
 constexpr int kJRowsPerLane = kJTileM / 64;
 constexpr int kJTileCols = kJWaves * kJNW;
@@ -251,7 +251,11 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
 #define TSG_JIT_A16 "v[122:137]"
 #define TSG_JIT_A8 "v[122:129]"
 #endif
-#if TSG_JIT_NW == 64
+#if TSG_JIT_NW == 128  // 8 waves only: v[116:244)
+    F32x32 a0 = {}, a1 = {}, a2 = {}, a3 = {};  // comp.h:41
+    TSG_JIT_CALL("+{v[116:147]}"(a0), "+{v[148:179]}"(a1), "+{v[180:211]}"(a2), "+{v[212:243]}"(a3));
+    auto acc_of = [&](int c, int) { return c < 32 ? a0[c] : c < 64 ? a1[c - 32] : c < 96 ? a2[c - 64] : a3[c - 96]; };
+#elif TSG_JIT_NW == 64
     F32x32 a0 = {}, a1 = {};  // comp.h:41
     TSG_JIT_CALL("+{" TSG_JIT_A0 "}"(a0), "+{" TSG_JIT_A1 "}"(a1));
     auto acc_of = [&](int c, int) { return c < 32 ? a0[c] : a1[c - 32]; };

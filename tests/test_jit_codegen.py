@@ -411,7 +411,7 @@ def test_jit_code_far_image(tsg, oracle_mod, M, K, N, s):
 
 @pytest.mark.parametrize("M,K,N,s", [(1, 1, 1, 1), (5, 70, 33, 2), (64, 200, 130, 4), (17, 300, 64, 8),
                                      (3, 97, 9, 16), (100, 390, 40, 4)])
-@pytest.mark.parametrize("width,waves", [(64, 8), (16, 4), (8, 8)])
+@pytest.mark.parametrize("width,waves", [(128, 8), (64, 8), (16, 4), (8, 8)])
 def test_jit_code_64row_image(tsg, oracle_mod, M, K, N, s, width, waves):
     """The 64-row image (one M row per lane, VOP2 v_add_f32 / v_sub_f32, k-quad
     X^T, 192-row chunks; tsg_internal.h): emulated workgroup by workgroup,
@@ -462,6 +462,10 @@ def test_jit_width_rejected(tsg, oracle_mod):
     t = O.tcsc_encode(O.gen_ternary(64, 20, 4, 1))
     with pytest.raises(tsg.TSGError, match="width"):
         tsg.jit_codegen(*t.arrays, 64, 20, width=24)
+    with pytest.raises(tsg.TSGError, match="width"):  # 128 columns per wave: the 64-row image only
+        tsg.jit_codegen(*t.arrays, 64, 20, width=128)
+    with pytest.raises(tsg.TSGError, match="shape"):  # ... with 8 waves
+        tsg.jit_codegen64(*t.arrays, 64, 20, width=128, waves=4)
     blk = O.blocked_tcsc_encode(O.gen_ternary(64, 20, 4, 1), 16)
     with pytest.raises(tsg.TSGError, match="BlockedTCSC"):
         tsg.jit_codegen(*blk, 64, 20, B=16, width=16)
@@ -588,9 +592,11 @@ def _rsrc1_of(co_path, symbol="tsg_jit_kernel.kd"):
     raise AssertionError(f"{symbol} not found in {co_path}")
 
 
-@pytest.mark.parametrize("co", ["tsg_jit.co", "tsg_jit_w32.co", "tsg_jit_w16.co", "tsg_jit_w8.co"])
+@pytest.mark.parametrize("co", ["tsg_jit.co", "tsg_jit_w32.co", "tsg_jit_w16.co", "tsg_jit_w8.co",
+                                "tsg_jit64_w128.co", "tsg_jit64_w64.co", "tsg_jit64_w16_4w.co"])
 def test_kernel_descriptor_float_mode(co):
-    rsrc1 = _rsrc1_of(os.path.join(_REPO_ROOT, "ternary-spgemm_amd", "lib", co))
+    sym = "tsg_jit64_kernel.kd" if co.startswith("tsg_jit64") else "tsg_jit_kernel.kd"
+    rsrc1 = _rsrc1_of(os.path.join(_REPO_ROOT, "ternary-spgemm_amd", "lib", co), sym)
     assert (rsrc1 >> 16) & 3 == 3, "FP32 denormals must be preserved (FLOAT_DENORM_MODE_32)"
     assert (rsrc1 >> 23) & 1 == 1, "IEEE mode must be on"
 
