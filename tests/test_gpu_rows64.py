@@ -37,11 +37,11 @@ def test_edges_rows64(tsg, oracle_mod, M, K, N, s):
     h.close()
 
 
-@pytest.mark.parametrize("width", [64, 32, 16, 8])
+@pytest.mark.parametrize("width", [128, 64, 32, 16, 8])
 @pytest.mark.parametrize("M,K", [(1, 191), (63, 192), (64, 193), (65, 385), (130, 1000), (37, 4096)])
 def test_rows64_widths_and_tiles(tsg, oracle_mod, width, M, K):
-    """Every stream width (8 waves when pinned), M across 64-row tiles and K
-    across 192-row chunks."""
+    """Every stream width (8 waves when pinned; 128 columns per wave only
+    here), M across 64-row tiles and K across 192-row chunks."""
     O = oracle_mod
     N = 700
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, width + M + K))
