@@ -433,7 +433,7 @@ def main():
             # committed rocprofv3 PMC passes (scripts/pmc_summary.py: FETCH_SIZE
             # and WRITE_SIZE with the gfx950 corrections of MI355X_MICROARCH.md)
             pm = json.load(open(PROFILE_PMC))
-            if pm.get("workload") == f"{M}x{K}x{Nr}s{s}":
+            if pm.get("workload") == f"{M}x{K}x{Nr}s{s}" and pm.get("kernel") == kname:
                 traffic = pm.get("kernels", {}).get(kname, {}).get("hbm_bytes")
         except Exception:
             pass

@@ -315,8 +315,18 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64 = false);
 // 2048 224 vs 245; K = 16384, N = 4096, M = 2048 806 vs 973); the 128-row
 // image keeps the calls its widest shape fills in whole rounds (configs[2]
 // 1360 vs 1437, N = 16384 M = 1024 339 vs 358, N = 8192 M = 4096 686 vs 708,
-// s = 8 / 16 862 / 637 vs 880 / 661).  tcsc_hip_set_tile_rows pins one;
-// TSG_JIT_ROWS64_MAXM replaces the rule by M <= its value (A/B).
+// s = 8 / 16 862 / 637 vs 880 / 661) -- against its 64-wide streams.  At 128
+// columns per wave (round 4, profiles/r04l_w128_ab.jsonl, kernel / step us)
+// the 64-row image wins those too wherever that shape is its modelled best:
+// configs[2] 1286 / 1329 vs 1350 / 1387, s = 8 748 / 790 vs 841 / 886, s = 16
+// 500 / 542 vs 609 / 651, N = 16384 M = 1024 320 / 337 vs 331 / 347, M =
+// 2048 643 / 664 vs 660 / 685, N = 8192 M = 4096 623 vs 655, configs[2] s = 2
+// 2403 vs 2465, (16000, 8192, 2048) 1219 vs 1302, (8192, 16384, 4096) 2467
+// vs 2833, (64000, 16384, 4096) s = 8 / 16 11.2 / 7.2 vs 14.3 / 8.7 ms (one
+// loss: M = N = K = 4096 361 vs 353); the far-X^T image and dense W over
+// long K stay 128-row.
+// tcsc_hip_set_tile_rows pins one; TSG_JIT_ROWS64_MAXM replaces the rule by
+// M <= its value (A/B).
 bool pick_rows64(const tsg_tcsc *h, int M)
 {
     static const int env_max = [] {
@@ -329,6 +339,16 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     if (env_max >= 0) return M <= env_max;
     if (M <= kRows64AutoMaxM) return true;
     const JitShape s = pick_jit_shape(h, M, false);
+    if (s.far) return false;  // the far-X^T image (long K, X^T past the Infinity Cache) is 128-row only
+    // dense W over long K: the 128-row image's long-stream map keeps each
+    // XCD on one column tile's code ((64000, 16384, 4096) s = 2: 39.0 vs
+    // 50.6 ms, profiles/r04m_w128_big.jsonl)
+    const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
+    if (h->K >= 8192 && density > 0.375) return false;
+    // 128 columns per wave fill whole rounds: twice the adds per staged chunk
+    // and per X read of either 64-wide stream (profiles/r04l_w128_ab.jsonl,
+    // r04m_w128_big.jsonl)
+    if (pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW) return true;
     if (s.nw != tsg::kJitNW || s.waves != tsg::kJitWaves) return true;
     const int64_t wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                         ((h->N + (int64_t)s.waves * s.nw - 1) / ((int64_t)s.waves * s.nw));
@@ -372,7 +392,6 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
         for (int nw : tsg::kJit64Widths)
             for (int waves : {tsg::kJitWaves, 4}) {
                 if (!tsg::jit_waves_ok(nw, waves)) continue;
-                if (nw == tsg::kJit64WideNW) continue;  // pinned only (tcsc_hip_set_jit_width) until measured
                 if (env_waves == 4 && nw < tsg::kJitNW && waves != 4) continue;
                 const int64_t ntile = (h->N + (int64_t)waves * nw - 1) / ((int64_t)waves * nw), wgs = mt * ntile;
                 const double image = image8 + (double)ntile * waves * h->jit_nch * 2 * (160.0 + 8.0 * tsg::kJitChunk);

@@ -7,23 +7,25 @@ import pytest
 
 
 @pytest.mark.parametrize("shape,plan", [
-    # configs[2] (the bench): 64 x 8, CU pairs on one code stream (2 x 16)
-    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(2, 16), tmask=0)),
+    # configs[2] (the bench): the 64-row image at 128 columns per wave, CU pairs on one code
+    # stream (2 x 16) (round 4, r04l_w128_ab.jsonl: 1286 / 1329 vs the 128-row 64 x 8 1350 / 1387 us)
+    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=0)),
     # configs[1]: the 64-row image, 16 x 8 one-round grid (two waves per SIMD), code touches
     # thinned (round 4, r04j_waves_ab.jsonl: kernel / step 79.6 / 95.5 us vs 32 x 4 92.8 / 108.4;
     # the 128-row image's 16 x 4 96.8-100.3 / 111.8-115.9, r04g)
     ((512, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(4, 8), tmask=3)),
-    # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt)
-    ((4096, 4096, 16384, 16), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=0)),
+    # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt), 128 x 8 64-row (500 vs 609 us, r04l)
+    ((4096, 4096, 16384, 16), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
     # the reference's largest case: s = 4 far-X^T image on 1 x 32 (r03e_far_ab.txt) ...
     ((64000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
-    # ... s = 2 (code past the Infinity Cache) and s = 8 default image on 1 x 32 (r03f_sparse_big_ab.txt) ...
+    # ... s = 2 (code past the Infinity Cache) 128-row on 1 x 32 (r03f_sparse_big_ab.txt; the 64-row
+    # image 50.6 vs 39.0 ms, r04m_w128_big.jsonl) ...
     ((64000, 16384, 4096, 2), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
-    ((64000, 16384, 4096, 8), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
-    # ... s = 16 on 4 x 8
-    ((64000, 16384, 4096, 16), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=0)),
-    # X^T too small for the far image (r03e_long_k_ab.txt) / large enough
-    ((8192, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
+    # ... s = 8 / 16 on the 64-row image's 128 x 8, 4 x 8 (11.2 / 7.2 vs 14.3 / 8.7 ms, r04m)
+    ((64000, 16384, 4096, 8), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
+    ((64000, 16384, 4096, 16), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
+    # X^T too small for the far image (r03e_long_k_ab.txt): 64-row 128 x 8 (2467 vs 2833 us, r04m) / large enough
+    ((8192, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
     ((16000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
     # the 64-row image at mid M (round 4, r04d_rows64_ab.jsonl): one round of workgroups,
     # the shape of least modelled time (tsg_capi.cpp pick_jit_shape)
@@ -36,11 +38,12 @@ import pytest
     # above M = 512 the 64-row image wherever the 128-row image's shape is narrower than
     # 64 x 8 or leaves a round partly empty (r04h_big_ab.jsonl, step us): M = 640 336 vs 385,
     # N = 4096 M = 1024 147 vs 160 (and (1024, 4096, 1024), r04i_plan_ab.jsonl) ...
-    ((640, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(2, 10), tmask=0)),
+    ((640, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 10), tmask=3)),
     ((1024, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(2, 16), tmask=3)),
     ((1024, 4096, 1024, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=4, far=False, map=(2, 16), tmask=3)),
-    # ... the 128-row image where 64 x 8 fills whole rounds: M = 1024 339 vs 358
-    ((1024, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=3)),
+    # ... and at 128 columns per wave where that fills rounds: M = 1024 320 / 337 vs the 128-row
+    # image's 331 / 347 (r04l_w128_ab.jsonl)
+    ((1024, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=3)),
 ])
 def test_plan_matches_measured_winners(tsg, shape, plan):
     M, K, N, s = shape
@@ -57,7 +60,7 @@ def test_plan_matches_measured_winners(tsg, shape, plan):
     (96, 4096, 16384, "tsg_jit64_kernel"),
     (512, 4096, 16384, "tsg_jit64_kernel"),
     (1536, 4096, 16384, "tsg_jit64_kernel"),      # 128-row 64 x 8 in 1.5 rounds (547 vs 617 us, r04h)
-    (2048, 4096, 16384, "tsg_jit_kernel"),        # ... in whole rounds (695 vs 697 us; configs[2] 1360 vs 1437)
+    (2048, 4096, 16384, "tsg_jit64_kernel"),      # 128 x 8 64-row (643 vs 660 us, r04l)
     (32, 1024, 4096, "tsg_tcsc_ell_kernel"),      # configs[0]
     (16, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 16 (184 vs 247 us, r04g)
     (17, 16384, 16384, "tsg_jit64_kernel"),       # (M = 32: 310 vs 248 us)
@@ -68,6 +71,14 @@ def test_plan_matches_measured_winners(tsg, shape, plan):
 ])
 def test_plan_small_m_kernel(tsg, M, K, N, kernel):
     assert tsg.call_plan(K, N, K * N // 4, M)["kernel"] == kernel
+
+
+def test_plan_dense_long_k_stays_128_row(tsg):
+    """Dense W (s = 2) over long K keeps the 128-row image's long-stream map
+    ((64000, 16384, 4096) s = 2: 39.0 vs 50.6 ms, profiles/r04m_w128_big.jsonl);
+    at K = 4096 the 64-row image takes s = 2 (2403 vs 2465 us)."""
+    assert tsg.call_plan(16384, 4096, 16384 * 4096 // 2, 4096)["kernel"] == "tsg_jit_kernel"
+    assert tsg.call_plan(4096, 16384, 4096 * 16384 // 2, 4096)["kernel"] == "tsg_jit64_kernel"
 
 
 def test_plan_rejects_bad_arguments(tsg):
