@@ -26,6 +26,7 @@ ap.add_argument("--M", default="1,8,16,32,48,64,96,128,192,256,512")
 ap.add_argument("--widths", default="0")
 ap.add_argument("--modes", default="ell,jit128,jit64")
 ap.add_argument("--reps", type=int, default=30)
+ap.add_argument("--xint", action="store_true", help="X integer U[-512, 512] (bench.py's X) instead of order-sensitive")
 a = ap.parse_args()
 import torch  # noqa: E402
 
@@ -55,10 +56,12 @@ def timed(M, X, Y):
 for M in (int(v) for v in a.M.split(",")):
     g = torch.Generator(device="cuda")
     g.manual_seed(12345)
-    # order-sensitive X: mantissas over an exponent spread (every partial sum rounds)
-    X = (torch.randint(-(1 << 23), 1 << 23, (M, a.K), generator=g, device="cuda", dtype=torch.int32).float()
-         * torch.exp2(-torch.randint(0, 24, (M, a.K), generator=g, device="cuda").float()))
-    out = {"M": M, "K": a.K, "N": a.N, "s": a.s, "waves_env": os.environ.get("TSG_JIT_WAVES"),
+    if a.xint:  # bench.py's X: small integers (exact partial sums, few toggling bits)
+        X = torch.randint(-512, 513, (M, a.K), generator=g, device="cuda", dtype=torch.int32).float()
+    else:  # order-sensitive X: mantissas over an exponent spread (every partial sum rounds)
+        X = (torch.randint(-(1 << 23), 1 << 23, (M, a.K), generator=g, device="cuda", dtype=torch.int32).float()
+             * torch.exp2(-torch.randint(0, 24, (M, a.K), generator=g, device="cuda").float()))
+    out = {"M": M, "K": a.K, "N": a.N, "s": a.s, "x": "int" if a.xint else "frac", "waves_env": os.environ.get("TSG_JIT_WAVES"),
            "xdirect_env": os.environ.get("TSG_JIT_XDIRECT"), "qblock_env": os.environ.get("TSG_JIT_QBLOCK")}
     ref = None
     for mode in a.modes.split(","):

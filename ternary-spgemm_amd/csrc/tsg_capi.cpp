@@ -347,8 +347,14 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     if (h->K >= 8192 && density > 0.375) return false;
     // 128 columns per wave fill whole rounds: twice the adds per staged chunk
     // and per X read of either 64-wide stream (profiles/r04l_w128_ab.jsonl,
-    // r04m_w128_big.jsonl)
-    if (pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW) return true;
+    // r04m_w128_big.jsonl) -- for sparse W or long K.  Dense W over short K
+    // depends on the data (r04o_xdata_ab.jsonl, kernel us): with bench.py's
+    // small-integer X the 128-row image is faster at configs[2] (1197 vs
+    // 1232), with full-mantissa X slower (1277 vs 1252) -- v_pk_add_f32 runs
+    // slower on high-entropy data, the VOP2 stream hardly -- so the 128-row
+    // image keeps it; the sparse end is the 64-row image's either way (s = 16:
+    // 468 vs 569 int, 496 vs 600 frac).
+    if ((density <= 0.1875 || h->K >= 8192) && pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW) return true;
     if (s.nw != tsg::kJitNW || s.waves != tsg::kJitWaves) return true;
     const int64_t wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                         ((h->N + (int64_t)s.waves * s.nw - 1) / ((int64_t)s.waves * s.nw));

@@ -7,14 +7,16 @@ import pytest
 
 
 @pytest.mark.parametrize("shape,plan", [
-    # configs[2] (the bench): the 64-row image at 128 columns per wave, CU pairs on one code
-    # stream (2 x 16) (round 4, r04l_w128_ab.jsonl: 1286 / 1329 vs the 128-row 64 x 8 1350 / 1387 us)
-    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=0)),
+    # configs[2] (the bench): 64 x 8, CU pairs on one code stream (2 x 16); the 128-row image
+    # with bench.py's integer X (1197 vs 1232 us for the 64-row 128 x 8; with full-mantissa X
+    # 1277 vs 1252, r04o_xdata_ab.jsonl)
+    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(2, 16), tmask=0)),
     # configs[1]: the 64-row image, 16 x 8 one-round grid (two waves per SIMD), code touches
     # thinned (round 4, r04j_waves_ab.jsonl: kernel / step 79.6 / 95.5 us vs 32 x 4 92.8 / 108.4;
     # the 128-row image's 16 x 4 96.8-100.3 / 111.8-115.9, r04g)
     ((512, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(4, 8), tmask=3)),
-    # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt), 128 x 8 64-row (500 vs 609 us, r04l)
+    # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt), 128 x 8 64-row (468 vs 569 us with
+    # integer X, 496 vs 600 fractional, r04o)
     ((4096, 4096, 16384, 16), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
     # the reference's largest case: s = 4 far-X^T image on 1 x 32 (r03e_far_ab.txt) ...
     ((64000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
@@ -41,9 +43,9 @@ import pytest
     ((640, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 10), tmask=3)),
     ((1024, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(2, 16), tmask=3)),
     ((1024, 4096, 1024, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=4, far=False, map=(2, 16), tmask=3)),
-    # ... and at 128 columns per wave where that fills rounds: M = 1024 320 / 337 vs the 128-row
-    # image's 331 / 347 (r04l_w128_ab.jsonl)
-    ((1024, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=3)),
+    # ... the 128-row image where 64 x 8 fills whole rounds and W is dense over short K (M = 1024
+    # 339 vs 358 us, r04h; the 64-row 128 x 8 ties: 342 vs 338 int, 355 vs 356 frac, r04o)
+    ((1024, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=3)),
 ])
 def test_plan_matches_measured_winners(tsg, shape, plan):
     M, K, N, s = shape
@@ -60,7 +62,7 @@ def test_plan_matches_measured_winners(tsg, shape, plan):
     (96, 4096, 16384, "tsg_jit64_kernel"),
     (512, 4096, 16384, "tsg_jit64_kernel"),
     (1536, 4096, 16384, "tsg_jit64_kernel"),      # 128-row 64 x 8 in 1.5 rounds (547 vs 617 us, r04h)
-    (2048, 4096, 16384, "tsg_jit64_kernel"),      # 128 x 8 64-row (643 vs 660 us, r04l)
+    (2048, 4096, 16384, "tsg_jit_kernel"),        # dense, short K, whole rounds (615 vs 617 us int, r04o)
     (32, 1024, 4096, "tsg_tcsc_ell_kernel"),      # configs[0]
     (16, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 16 (184 vs 247 us, r04g)
     (17, 16384, 16384, "tsg_jit64_kernel"),       # (M = 32: 310 vs 248 us)
@@ -76,9 +78,10 @@ def test_plan_small_m_kernel(tsg, M, K, N, kernel):
 def test_plan_dense_long_k_stays_128_row(tsg):
     """Dense W (s = 2) over long K keeps the 128-row image's long-stream map
     ((64000, 16384, 4096) s = 2: 39.0 vs 50.6 ms, profiles/r04m_w128_big.jsonl);
-    at K = 4096 the 64-row image takes s = 2 (2403 vs 2465 us)."""
+    s = 4 over long K takes the 64-row image's 128 x 8 ((8192, 16384, 4096):
+    2484 vs 2453 us int, 2476 vs 2833 frac, r04o_xdata_ab.jsonl)."""
     assert tsg.call_plan(16384, 4096, 16384 * 4096 // 2, 4096)["kernel"] == "tsg_jit_kernel"
-    assert tsg.call_plan(4096, 16384, 4096 * 16384 // 2, 4096)["kernel"] == "tsg_jit64_kernel"
+    assert tsg.call_plan(16384, 4096, 16384 * 4096 // 4, 8192)["kernel"] == "tsg_jit64_kernel"
 
 
 def test_plan_rejects_bad_arguments(tsg):
