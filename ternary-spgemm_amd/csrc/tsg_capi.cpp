@@ -112,6 +112,8 @@ constexpr int kEllTile8 = 2;
 constexpr int kEllMidM = 32;
 constexpr int64_t kEllPcRowsMaxMN = 32768;
 constexpr int kEllStarvedMaxM = 1024;
+constexpr int kEllSmallWMaxM = 128;          // small W: the walk up to this M ...
+constexpr double kEllSmallWWork = 420e6;     // ... while M x nnz stays below this
 // M up to which the automatic choice always takes the 64-row image, and the
 // filled fraction of its last round below which the 128-row image's widest
 // shape loses to it (pick_rows64)
@@ -632,11 +634,20 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     const int64_t jit_wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                             ((h->N + 8 * tsg::kJitWaves - 1) / (8 * tsg::kJitWaves));
     const bool starved = one8 && M <= kEllStarvedMaxM && jit_wgs <= kEllStarvedWgs;
-    static const int auto_max = [] {  // TSG_ELL_MAXM: A/B of the small-M boundary
-        const char *e = tsg::knob_value("TSG_ELL_MAXM");
-        return e ? atoi(e) : kEllAutoMaxM;
-    }();
-    if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) && !starved) return -1;
+    static const char *env_max = tsg::knob_value("TSG_ELL_MAXM");  // A/B of the small-M boundary
+    const int auto_max = env_max ? atoi(env_max) : kEllAutoMaxM;
+    // a small W (M x nnz <= 420 M) keeps the walk up to M = 128 while K fits
+    // one chunk: the 64-row image streams its whole code image and stages X
+    // (~13 us of step overhead against ~6) whatever M is, the walk's cost
+    // grows with M x nnz (profiles/r04r_sparse_small_ab.jsonl, step us:
+    // (64, 2048, 8192) s = 8 26.6 vs 36.9, s = 16 21.7 vs 35.2, s = 4 35.9 vs
+    // 41.0; (96, 4096, 16384) s = 16 61.3 vs 77.9; beyond it the image wins:
+    // (128, 4096, 16384) s = 16 80.3 vs 76.1, (64, 4096, 16384) s = 8 66.2 vs
+    // 63.0, s = 4 at M = 48 101 vs 71)
+    const bool small_w = !env_max && one8 && M <= kEllSmallWMaxM &&
+                         (double)M * (double)(h->nnz_pos + h->nnz_neg) <= kEllSmallWWork;
+    if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) && !starved && !small_w)
+        return -1;
     int v = 0;
     if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
         v = kEllTile8;

@@ -76,6 +76,20 @@ def test_plan_small_m_kernel(tsg, M, K, N, kernel):
     assert tsg.call_plan(K, N, K * N // 4, M)["kernel"] == kernel
 
 
+@pytest.mark.parametrize("M,K,N,s,kernel", [
+    # small W (M x nnz <= 420 M, K in one chunk): the walk up to M = 128 (r04r_sparse_small_ab.jsonl, step us)
+    (64, 2048, 8192, 8, "tsg_tcsc_ell_kernel"),   # 26.6 vs 36.9
+    (64, 2048, 8192, 16, "tsg_tcsc_ell_kernel"),  # 21.7 vs 35.2
+    (64, 2048, 8192, 4, "tsg_tcsc_ell_kernel"),   # 35.9 vs 41.0
+    (96, 4096, 16384, 16, "tsg_tcsc_ell_kernel"),  # 61.3 vs 77.9
+    (128, 4096, 16384, 16, "tsg_jit64_kernel"),   # 76.1 vs 80.3
+    (64, 4096, 16384, 8, "tsg_jit64_kernel"),     # 63.0 vs 66.2
+    (64, 2048, 8192, 2, "tsg_jit64_kernel"),      # reference case: 36.3 vs 50.2 kernel (r04q_ref_cases.jsonl)
+])
+def test_plan_small_w_walk(tsg, M, K, N, s, kernel):
+    assert tsg.call_plan(K, N, K * N // s, M)["kernel"] == kernel
+
+
 def test_plan_dense_long_k_stays_128_row(tsg):
     """Dense W (s = 2) over long K keeps the 128-row image's long-stream map
     ((64000, 16384, 4096) s = 2: 39.0 vs 50.6 ms, profiles/r04m_w128_big.jsonl);
