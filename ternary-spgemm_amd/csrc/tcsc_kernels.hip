@@ -121,52 +121,39 @@ __global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *_
 // PR rows per piece (16 or 8) and Q = 64 / PR quads: the 1-KiB piece pr = Q qg
 // + rg of (chunk c, M tile t) at ((c * Mt + t) * 48 + pr) KiB holds, in 16-B
 // lane slot j, X[64 t + PR rg + j % PR][4 (48 c + Q qg + j / PR) .. +3] -- zero
-// past M or K -- so the kernel's DMA pieces are coalesced 1-KiB reads.  A 64 x
-// 64 tile of X (64 rows x 16 quads of one chunk) is read along k (coalesced
-// rows) into LDS, then written as 16 whole pieces.
+// past M or K -- so the kernel's DMA pieces are coalesced 1-KiB reads.  Every
+// slot is 16 contiguous bytes of a row of X, so this is a gather-copy, not a
+// transpose: one wave writes one whole piece (1 KiB, one store per lane) from
+// PR row segments of 1024 / PR bytes (the other half of a PR = 16 segment's
+// 128-B line is the next piece's, copied by the neighbouring workgroup); no
+// LDS, no barrier.  A workgroup copies 4 consecutive pieces of one (chunk, M
+// tile).  HBM-bound: 8 * Mp * Kp bytes.
 template <bool VEC, int PR>
 __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *__restrict__ X,
                                                                   float *__restrict__ XQ, int M, int K,
                                                                   int Mp, int Kp)
 {
-    __shared__ float tile[64][65];  // [m][k]
-    const int k0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
-    if (VEC) {
-        const int c4 = (threadIdx.x & 15) * 4, r = threadIdx.x >> 4;  // 16 x 16
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int ml = r + 16 * i, m = m0 + ml, k = k0 + c4;
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (m < M && k < K) v = *reinterpret_cast<const float4 *>(X + (size_t)m * K + k);  // K % 4 == 0
-            tile[ml][c4] = v.x;
-            tile[ml][c4 + 1] = v.y;
-            tile[ml][c4 + 2] = v.z;
-            tile[ml][c4 + 3] = v.w;
-        }
-    } else {
-        const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int m = m0 + ty + 4 * i, k = k0 + tx;
-            tile[ty + 4 * i][tx] = (m < M && k < K) ? X[(size_t)m * K + k] : 0.0f;
-        }
-    }
-    __syncthreads();
-    // thread t writes lane slot j = t % 64 of the tile's piece p = 4 i + t / 64
-    // (quad group p / Q, row group p % Q): row PR rg + j % PR, quad Q qg + j / PR
-    // -- 256 threads = 4 whole pieces per i, 16 per tile
     constexpr int Q = 64 / PR;
-    const int j = threadIdx.x & 63;
-    const int c = k0 / 192, mt = m0 >> 6, Mt = Mp >> 6;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int p = 4 * i + (threadIdx.x >> 6), qgl = p / Q, rg = p % Q, ml = rg * PR + (j % PR);
-        const int kk = 4 * (Q * qgl + j / PR);               // k within the tile
-        const int qg = (k0 % 192) / (4 * Q) + qgl;           // quad group within the chunk
-        const size_t piece = ((size_t)c * Mt + mt) * 48 + (size_t)(Q * qg + rg);
-        *reinterpret_cast<float4 *>(XQ + piece * 256 + (size_t)j * 4) =
-            make_float4(tile[ml][kk], tile[ml][kk + 1], tile[ml][kk + 2], tile[ml][kk + 3]);
+    const int Mt = Mp >> 6;
+    const int blk = blockIdx.x;                     // (chunk * Mt + t) * 12 + piece group
+    const int ct = blk / 12, pr = (blk % 12) * 4 + (threadIdx.x >> 6);
+    const int c = ct / Mt, t = ct % Mt, j = threadIdx.x & 63;
+    const int qg = pr / Q, rg = pr % Q;
+    const int m = 64 * t + PR * rg + (j % PR);
+    const int k = 4 * (48 * c + Q * qg + j / PR);
+    float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (m < M) {
+        const float *row = X + (size_t)m * K;
+        if (VEC) {
+            if (k < K) v = *reinterpret_cast<const float4 *>(row + k);  // K % 4 == 0: whole quad inside
+        } else {
+            if (k < K) v.x = row[k];
+            if (k + 1 < K) v.y = row[k + 1];
+            if (k + 2 < K) v.z = row[k + 2];
+            if (k + 3 < K) v.w = row[k + 3];
+        }
     }
+    *reinterpret_cast<float4 *>(XQ + ((size_t)ct * 48 + pr) * 256 + (size_t)j * 4) = v;
 }
 
 // One LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS
@@ -340,9 +327,12 @@ int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int 
 int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream)
 {
     // Mp is a multiple of 64 (the 64-row image's M tile) and Kp of 192 (its
-    // chunk): the 64 x 64 tiles cover [0, Kp) x [0, Mp) exactly, three per chunk
+    // chunk): the pieces cover [0, Kp) x [0, Mp) exactly
     if (Mp % 64 || Kp % 192) return -1;
-    dim3 grid((unsigned)(Kp / 64), (unsigned)(Mp / 64));
+    // 12 workgroups of 4 pieces per (chunk, M tile)
+    const int64_t blocks = (int64_t)(Kp / 192) * (Mp / 64) * 12;
+    if (blocks >= ((int64_t)1 << 31)) return -1;
+    dim3 grid((unsigned)blocks);
     const bool vec = K % 4 == 0 && ((uintptr_t)X & 15) == 0;
     hipStream_t s = (hipStream_t)stream;
     if (piece_rows == 16) {
