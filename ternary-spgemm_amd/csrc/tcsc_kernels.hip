@@ -134,10 +134,14 @@ __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *_
                                                                   int Mp, int Kp)
 {
     constexpr int Q = 64 / PR;
-    const int Mt = Mp >> 6;
-    const int blk = blockIdx.x;                     // (chunk * Mt + t) * 12 + piece group
-    const int ct = blk / 12, pr = (blk % 12) * 4 + (threadIdx.x >> 6);
-    const int c = ct / Mt, t = ct % Mt, j = threadIdx.x & 63;
+    const int Mt = Mp >> 6, nch = Kp / 192;
+    // workgroup order (M tile * nch + chunk) * 12 + piece group: the workgroups
+    // in flight read a few M tiles' rows end to end (long runs of each row), not
+    // one chunk of every row
+    const int blk = blockIdx.x;
+    const int tc = blk / 12, pr = (blk % 12) * 4 + (threadIdx.x >> 6);
+    const int t = tc / nch, c = tc % nch, j = threadIdx.x & 63;
+    const int ct = c * Mt + t;
     const int qg = pr / Q, rg = pr % Q;
     const int m = 64 * t + PR * rg + (j % PR);
     const int k = 4 * (48 * c + Q * qg + j / PR);
