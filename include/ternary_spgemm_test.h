@@ -36,8 +36,9 @@ int64_t tcsc_hip_call_image_bytes(tsg_tcsc *h, int M);
  * workgroups fill the GPU -- each width is its own code image, compiled on the
  * first call (or tcsc_hip_reserve) that picks it.  Same results bit for bit.
  * tcsc_hip_jit_width: the width a call with M rows runs (0: not a jit handle).
- * tcsc_hip_set_jit_width: 0 = automatic (default), or pin 64/32/16/8
- * (BlockedTCSC: 64 only).  Extension: no reference counterpart. */
+ * tcsc_hip_set_jit_width: 0 = automatic (default), or pin 64/32/16/8, or
+ * 128 (the 64-row image only: pinning it selects that image; BlockedTCSC: 64
+ * only).  Extension: no reference counterpart. */
 int tcsc_hip_jit_width(const tsg_tcsc *h, int M);
 int tcsc_hip_set_jit_width(tsg_tcsc *h, int width);
 /* Waves per workgroup of that call's image: 8, or 4 (narrow widths at mid M:
@@ -45,8 +46,9 @@ int tcsc_hip_set_jit_width(tsg_tcsc *h, int width);
 int tcsc_hip_jit_waves(const tsg_tcsc *h, int M);
 
 /* Small-M kernel (no reference counterpart; DESIGN.md 4 "Small M"): calls
- * with few rows (GEMV-like: M <= 64 when K fits an 8-row LDS chunk, else
- * M <= 16) on a plain-TCSC handle run an index-reading sliced-ELL walk
+ * with few rows (GEMV-like: M <= 32 when K fits an 8-row LDS chunk -- up to
+ * 128 for a small W, M x nnz <= 420 M -- else M <= 16, and grids the jit
+ * kernel cannot fill) on a plain-TCSC handle run an index-reading sliced-ELL walk
  * (tsg_tcsc_ell_kernel; tsg_tcsc_ell_pc_kernel, a producer/consumer split of
  * it, for M = 1) that reads X in place and streams its entry stream from HBM
  * once per M tile, instead of the weight-compiled kernel.  Same results bit
@@ -131,13 +133,16 @@ int tsg_ell_build(const int32_t *col_start_pos, const int32_t *col_start_neg, co
  * X^T in the k-quad layout.  Same results bit for bit.  rows: 0 = automatic
  * (default), 64 = the 64-row image, 128 = the 128-row image (v_pk_add_f32) for
  * every weight-compiled call (plain TCSC only).  tcsc_hip_call_tile_rows: the
- * M tile (64 / 128) of a call with M rows, 0 if it runs a small-M walk. */
+ * M tile (64 / 128) of a call with M rows, 0 if it runs a small-M walk.
+ * Which image is faster can depend on X itself: with
+ * full-mantissa activations, dense W and large M, 64 can beat the automatic
+ * choice by a few percent. */
 int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows);
 int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M);
 
 /* The 64-row image's machine code (layout as tsg_jit_codegen; region header
- * word 7 format 3, the k-quad layout): width 64 / 32 / 16 / 8, waves 8 (or 4
- * for the narrow widths). */
+ * word 7 format 3, the k-quad layout): width 128 / 64 / 32 / 16 / 8, waves 8
+ * (or 4 for widths 32, 16, 8). */
 int tsg_jit_codegen64(const int32_t *col_start_pos, const int32_t *col_start_neg,
                       const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
                       int width, int waves, uint32_t *code, int64_t code_cap, int64_t *code_len,
