@@ -147,6 +147,13 @@ int tsg_jit_codegen64(const int32_t *col_start_pos, const int32_t *col_start_neg
                       const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
                       int width, int waves, uint32_t *code, int64_t code_cap, int64_t *code_len,
                       uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+/* Its half ring (4-wave workgroups, widths 32 / 16 / 8; 96-row chunks, a
+ * 72-KiB ring so two workgroups share a CU; region header word 7 bit 19;
+ * TSG_JIT_HALF=1 selects it for the 4-wave calls, A/B). */
+int tsg_jit_codegen64h(const int32_t *col_start_pos, const int32_t *col_start_neg,
+                       const int32_t *row_index_pos, const int32_t *row_index_neg, int K, int N,
+                       int width, uint32_t *code, int64_t code_cap, int64_t *code_len,
+                       uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
 
 /* The environment knobs (csrc/tsg_knobs.cpp): "" when every set TSG_* knob
  * has an accepted value, else the error registration reports (a set

@@ -119,7 +119,8 @@ __global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *_
 
 // X [M][K] -> the blocked k-quad layout of the 64-row image (tsg_internal.h),
 // PR rows per piece (16 or 8) and Q = 64 / PR quads: the 1-KiB piece pr = Q qg
-// + rg of (chunk c, M tile t) at ((c * Mt + t) * 48 + pr) KiB holds, in 16-B
+// + rg of (chunk c, M tile t) at ((c * Mt + t) * U + pr) KiB (U = 48 units per
+// chunk, 24 for the half ring) holds, in 16-B
 // lane slot j, X[64 t + PR rg + j % PR][4 (48 c + Q qg + j / PR) .. +3] -- zero
 // past M or K -- so the kernel's DMA pieces are coalesced 1-KiB reads.  Every
 // slot is 16 contiguous bytes of a row of X, so this is a gather-copy, not a
@@ -131,20 +132,21 @@ __global__ __launch_bounds__(256) void tsg_transpose_pairs_kernel(const float *_
 template <bool VEC, int PR>
 __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *__restrict__ X,
                                                                   float *__restrict__ XQ, int M, int K,
-                                                                  int Mp, int Kp)
+                                                                  int Mp, int Kp, int units)
 {
+    // units: 1-KiB pieces per (chunk, M tile) -- 48, or 24 for the half ring
     constexpr int Q = 64 / PR;
-    const int Mt = Mp >> 6, nch = Kp / 192;
+    const int Mt = Mp >> 6, nch = Kp / (4 * units), groups = units / 4;
     // workgroup order (M tile * nch + chunk) * 12 + piece group: the workgroups
     // in flight read a few M tiles' rows end to end (long runs of each row), not
     // one chunk of every row
     const int blk = blockIdx.x;
-    const int tc = blk / 12, pr = (blk % 12) * 4 + (threadIdx.x >> 6);
+    const int tc = blk / groups, pr = (blk % groups) * 4 + (threadIdx.x >> 6);
     const int t = tc / nch, c = tc % nch, j = threadIdx.x & 63;
     const int ct = c * Mt + t;
     const int qg = pr / Q, rg = pr % Q;
     const int m = 64 * t + PR * rg + (j % PR);
-    const int k = 4 * (48 * c + Q * qg + j / PR);
+    const int k = 4 * (units * c + Q * qg + j / PR);
     float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (m < M) {
         const float *row = X + (size_t)m * K;
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *_
             if (k + 3 < K) v.w = row[k + 3];
         }
     }
-    *reinterpret_cast<float4 *>(XQ + ((size_t)ct * 48 + pr) * 256 + (size_t)j * 4) = v;
+    *reinterpret_cast<float4 *>(XQ + ((size_t)ct * units + pr) * 256 + (size_t)j * 4) = v;
 }
 
 // One LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS
@@ -328,23 +330,25 @@ int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream)
+int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream,
+                           int chunk)
 {
     // Mp is a multiple of 64 (the 64-row image's M tile) and Kp of 192 (its
     // chunk): the pieces cover [0, Kp) x [0, Mp) exactly
-    if (Mp % 64 || Kp % 192) return -1;
-    // 12 workgroups of 4 pieces per (chunk, M tile)
-    const int64_t blocks = (int64_t)(Kp / 192) * (Mp / 64) * 12;
+    if ((chunk != 192 && chunk != 96) || Mp % 64 || Kp % chunk) return -1;
+    // chunk / 16 workgroups of 4 pieces per (chunk, M tile)
+    const int units = chunk / 4;
+    const int64_t blocks = (int64_t)(Kp / chunk) * (Mp / 64) * (units / 4);
     if (blocks >= ((int64_t)1 << 31)) return -1;
     dim3 grid((unsigned)blocks);
     const bool vec = K % 4 == 0 && ((uintptr_t)X & 15) == 0;
     hipStream_t s = (hipStream_t)stream;
     if (piece_rows == 16) {
-        if (vec) hipLaunchKernelGGL((tsg_transpose_quads_kernel<true, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
-        else hipLaunchKernelGGL((tsg_transpose_quads_kernel<false, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
+        if (vec) hipLaunchKernelGGL((tsg_transpose_quads_kernel<true, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp, units);
+        else hipLaunchKernelGGL((tsg_transpose_quads_kernel<false, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp, units);
     } else if (piece_rows == 8) {
-        if (vec) hipLaunchKernelGGL((tsg_transpose_quads_kernel<true, 8>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
-        else hipLaunchKernelGGL((tsg_transpose_quads_kernel<false, 8>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp);
+        if (vec) hipLaunchKernelGGL((tsg_transpose_quads_kernel<true, 8>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp, units);
+        else hipLaunchKernelGGL((tsg_transpose_quads_kernel<false, 8>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp, units);
     } else {
         return -1;
     }

@@ -48,12 +48,14 @@ struct tsg_tcsc {
     struct JitVariant {
         int nw = 0, waves = 0, Npad = 0;
         int piece_rows = 0;               // 64-row image: rows per DMA piece (its X^T layout)
+        int nch = 0, chunk = 0;           // X^T chunks of the image and K rows per chunk
         tsg::JitModule mod;               // dispatcher + generated code, loaded
         uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
         int64_t code_bytes = 0, wcode_words = 0;
     };
     JitVariant jv[8];                     // 7: the 64 x 8 "far X^T" image (pick_jit_shape)
     JitVariant jv64[8];                   // the 64-row image (tsg_internal.h), shape_index 0..7
+    JitVariant jv64h[3];                  // its half ring (kJit64HalfChunk): 4-wave widths 32, 16, 8
     int jit_nch = 0;                      // X^T chunks (all widths)
     int jit64_nch = 0;                    // X^T chunks of the 64-row image (192 rows each)
     int tile_rows = 0;                    // tcsc_hip_set_tile_rows: 0 auto, 128 or 64 (jit images)
@@ -153,23 +155,24 @@ int check_device(int dev)
 
 // X^T dimensions of a call with M rows: rows padded to the M tile, K to
 // whole chunks (64-row image: k-quad layout, 64-row tiles, 192-row chunks)
-int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp, bool r64 = false)
+int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp, bool r64 = false, bool half = false)
 {
     const bool jit = h->kind == tsg_tcsc::kJit;
     const int tm = !jit ? tsg::kRxTileM : r64 ? tsg::kJit64TileM : tsg::kJitTileM;
     Mp = ((std::max(M, 1) + tm - 1) / tm) * tm;
-    const int nch64 = std::max(1, (h->K + tsg::kJit64Chunk - 1) / tsg::kJit64Chunk);
-    Kp = !jit ? h->rimg.nch * tsg::kRxChunk : r64 ? nch64 * tsg::kJit64Chunk : h->jit_nch * tsg::kJitChunk;
+    const int c64 = half ? tsg::kJit64HalfChunk : tsg::kJit64Chunk;
+    const int nch64 = std::max(1, (h->K + c64 - 1) / c64);
+    Kp = !jit ? h->rimg.nch * tsg::kRxChunk : r64 ? nch64 * c64 : h->jit_nch * tsg::kJitChunk;
     return TSG_OK;
 }
 
 // Grows the X^T work buffer (grow-only).  A grow frees the old buffer, so it
 // first waits for every launch that may still read it; it cannot happen while
 // a stream is being captured (tcsc_hip_reserve(max_M) before the capture).
-int ensure_work(tsg_tcsc *h, int M, bool capturing, bool r64 = false)
+int ensure_work(tsg_tcsc *h, int M, bool capturing, bool r64 = false, bool half = false)
 {
     int Mp, Kp;
-    dims_for(h, M, Mp, Kp, r64);
+    dims_for(h, M, Mp, Kp, r64, half);
     const size_t need = (size_t)Mp * Kp * sizeof(float);
     if (need <= h->work_bytes) return TSG_OK;
     if (capturing)
@@ -237,11 +240,13 @@ struct JitShape {
     int nw, waves;
     bool far = false;  // the far-X^T code image (tsg_jit.cpp build_jit_code)
     bool r64 = false;  // the 64-row image (tsg_internal.h)
+    bool half = false; // its half ring (4-wave shapes; tsg_internal.h kJit64HalfChunk)
 };
 int shape_index(const JitShape &sh) { return shape_index(sh.nw, sh.waves, sh.far && !sh.r64); }
 
 tsg_tcsc::JitVariant &variant_of(tsg_tcsc *h, const JitShape &sh)
 {
+    if (sh.r64 && sh.half) return h->jv64h[width_index(sh.nw) - 1];
     return sh.r64 ? h->jv64[shape_index(sh.nw, sh.waves)] : h->jv[shape_index(sh)];
 }
 
@@ -376,10 +381,13 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
         return e ? atoi(e) : 0;
     }();
     if (h->B) return {tsg::kJitNW, tsg::kJitWaves};
+    // the 64-row image's half ring for its 4-wave shapes (TSG_JIT_HALF=1, read per call: A/B)
+    const char *hv = r64 ? tsg::knob_value("TSG_JIT_HALF") : nullptr;
+    const bool half_on = hv && hv[0] == '1';
     if (h->jit_force) {
         const int f = !r64 && h->jit_force == tsg::kJit64WideNW ? tsg::kJitNW : h->jit_force;
         const int w = env_waves == 4 && tsg::jit_waves_ok(f, 4) ? 4 : tsg::kJitWaves;
-        return {f, w, !r64 && f == tsg::kJitNW && w == tsg::kJitWaves && far_xt(h, M), r64};
+        return {f, w, !r64 && f == tsg::kJitNW && w == tsg::kJitWaves && far_xt(h, M), r64, r64 && w == 4 && half_on};
     }
     const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM;
     const int64_t mt = (std::max(M, 1) + tile_m - 1) / tile_m;
@@ -418,6 +426,7 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
                     pick = {nw, waves, false, true};
                 }
             }
+        pick.half = pick.waves == 4 && half_on;
         return pick;
     }
     JitShape best{tsg::kJitNW, tsg::kJitWaves}, most{tsg::kJitNW, tsg::kJitWaves};
@@ -510,17 +519,18 @@ int handle_stream(tsg_tcsc *h, hipStream_t &s)
 // stream, or the handle's own non-blocking stream (nullptr) -- and
 // synchronises that stream only.  Caller holds h->mu (or owns h exclusively).
 int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStream_t s = nullptr, bool far = false,
-                       bool r64 = false)
+                       bool r64 = false, bool half = false)
 {
     const int i = shape_index(nw, waves, far && !r64);
-    if (i < 0 || !(r64 ? tsg::jit64_width_ok(nw) : tsg::jit_width_ok(nw)) || (r64 && (far || h->B)))
+    if (i < 0 || !(r64 ? tsg::jit64_width_ok(nw) : tsg::jit_width_ok(nw)) || (r64 && (far || h->B)) ||
+        (half && (!r64 || waves != 4 || nw >= tsg::kJitNW)))
         return fail(TSG_ERR_ARG, "unsupported jit stream width " + std::to_string(nw) + " x " + std::to_string(waves) +
-                                 " waves" + (r64 ? " (64-row image)" : ""));
-    tsg_tcsc::JitVariant &v = r64 ? h->jv64[i] : h->jv[i];
+                                 " waves" + (r64 ? (half ? " (64-row image, half ring)" : " (64-row image)") : ""));
+    tsg_tcsc::JitVariant &v = half ? h->jv64h[width_index(nw) - 1] : r64 ? h->jv64[i] : h->jv[i];
     if (v.mod.function) return TSG_OK;
     tsg::JitImage img;
     tsg::build_jit_code(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
-                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw, waves, far, r64);
+                        h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, h->B, img, nw, waves, far, r64, half);
     // stream offsets (wcode) and the dispatcher's region literal are 32-bit
     if ((uint64_t)img.code.size() * 4 >= (1ull << 32) - (1ull << 20))
         return fail(TSG_ERR_RANGE, "jit image of " + std::to_string((uint64_t)img.code.size() * 4) +
@@ -585,9 +595,11 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
     v.waves = waves;
     v.Npad = img.Npad;
     v.piece_rows = img.piece_rows;
+    v.nch = img.nch;
+    v.chunk = img.chunk;
     v.code_bytes = (int64_t)img.code.size() * 4;
     v.wcode_words = (int64_t)img.wcode.size();
-    (r64 ? h->jit64_nch : h->jit_nch) = img.nch;
+    if (!half) (r64 ? h->jit64_nch : h->jit_nch) = img.nch;
     return TSG_OK;
 }
 
@@ -756,17 +768,19 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         return TSG_OK;
     }
     const bool r64 = pick_rows64(h, M);
-    const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM, chunk = r64 ? tsg::kJit64Chunk : tsg::kJitChunk;
+    const JitShape sh = h->kind == tsg_tcsc::kJit ? pick_jit_shape(h, M, r64) : JitShape{0, 0};
+    const bool half = sh.half;
+    const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM,
+              chunk = r64 ? (half ? tsg::kJit64HalfChunk : tsg::kJit64Chunk) : tsg::kJitChunk;
     int Mp, Kp;
-    dims_for(h, M, Mp, Kp, r64);
+    dims_for(h, M, Mp, Kp, r64, half);
     tsg_tcsc::JitVariant *jv = nullptr;
     if (h->kind == tsg_tcsc::kJit) {
-        const JitShape sh = pick_jit_shape(h, M, r64);
         jv = &variant_of(h, sh);
         if (!jv->mod.function && capturing)
             return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(sh.nw) +
                                          " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
-        rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far, r64);
+        rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far, r64, half);
         if (rc) return rc;
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
@@ -778,7 +792,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     // buffer) when every row starts 16-B aligned and the offsets fit 32 bits
     const bool direct = r64 && x_direct(dX, M, K, jv->piece_rows);
     if (!direct) {
-        rc = ensure_work(h, M, capturing, r64);
+        rc = ensure_work(h, M, capturing, r64, half);
         if (rc) return rc;
     }
     // X^T of the previous call may still be read by its kernel on another
@@ -790,7 +804,8 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         // no X at all: chain is +0; X^T stays zero
         HIP_TRY(hipMemsetAsync(h->d_work, 0, (size_t)Mp * Kp * sizeof(float), s));
     } else if ((h->kind != tsg_tcsc::kJit ? tsg::launch_transpose(dX, h->d_work, M, K, Mp, Kp, s)
-                : r64                      ? tsg::launch_transpose_quads(dX, h->d_work, M, K, Mp, Kp, jv->piece_rows, s)
+                : r64                      ? tsg::launch_transpose_quads(dX, h->d_work, M, K, Mp, Kp, jv->piece_rows, s,
+                                                                         chunk)
                                            : tsg::launch_transpose_pairs(dX, h->d_work, M, K, Mp, Kp, s)) != 0) {
         return fail(TSG_ERR_HIP, std::string("transpose launch: ") + hipGetErrorString(hipGetLastError()));
     }
@@ -806,7 +821,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask);
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
-                               r64 ? h->jit64_nch : h->jit_nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
+                               jv->nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
                                jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
@@ -1016,8 +1031,9 @@ void free_handle(tsg_tcsc *h)
     for (void *p : {(void *)h->d_seg, (void *)h->d_ent, (void *)h->d_work, (void *)h->d_x,
                     (void *)h->d_b, (void *)h->d_y, (void *)h->d_alpha, (void *)h->d_status})
         if (p) (void)hipFree(p);
-    for (auto *vs : {&h->jv[0], &h->jv64[0]})
-        for (size_t i = 0; i < (vs == &h->jv[0] ? std::size(h->jv) : std::size(h->jv64)); i++) {
+    for (auto *vs : {&h->jv[0], &h->jv64[0], &h->jv64h[0]})
+        for (size_t i = 0; i < (vs == &h->jv[0] ? std::size(h->jv) : vs == &h->jv64[0] ? std::size(h->jv64)
+                                                                                      : std::size(h->jv64h)); i++) {
             if (vs[i].d_wcode) (void)hipFree(vs[i].d_wcode);
             vs[i].mod.unload();
         }
@@ -1295,7 +1311,7 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
             if (pick_ell_variant(h, m) >= 0) continue;  // the small-M kernel (its images below)
             const bool r64 = pick_rows64(h, m);
             const JitShape sh = pick_jit_shape(h, m, r64);
-            rc = ensure_jit_variant(h, sh.nw, sh.waves, nullptr, sh.far, r64);
+            rc = ensure_jit_variant(h, sh.nw, sh.waves, nullptr, sh.far, r64, sh.half);
             if (rc) return rc;
         }
     }
@@ -1513,6 +1529,7 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     int64_t jit_bytes = 0;
     for (const auto &v : h->jv) jit_bytes += v.code_bytes + v.wcode_words * 4;
     for (const auto &v : h->jv64) jit_bytes += v.code_bytes + v.wcode_words * 4;
+    for (const auto &v : h->jv64h) jit_bytes += v.code_bytes + v.wcode_words * 4;
     for (const auto &e : h->ell) jit_bytes += e.bytes;
     o->image_bytes = jit ? jit_bytes : (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;

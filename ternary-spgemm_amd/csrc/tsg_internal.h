@@ -132,6 +132,14 @@ constexpr uint32_t kJit64Format = 3;                    // region header word 7 
 // conflicts on ds_read_b128).  TSG_JIT_QBLOCK=16|8 picks (A/B).
 constexpr uint32_t kJit64R16Flag = 1u << 18;
 int jit64_piece_rows();  // 16 (default) or 8 (TSG_JIT_QBLOCK=8); tsg_jit.cpp
+// Half ring (64-row image, 4-wave workgroups only; region header word 7 bit
+// 19): 96-row chunks of 24 pieces (24 KiB), a 72-KiB ring, so two workgroups
+// share a CU and each SIMD runs two waves (a lone wave issues its VOP2 adds
+// at half rate); the 8-wave register contract (6 pieces per wave).  Staged
+// copy: piece (chunk c, M tile t, pr) at ((c * Mt + t) * 24 + pr) KiB.
+// Dispatchers lib/tsg_jit64h_w<nw>.co (TSG_JIT_HALF=1).
+constexpr int kJit64HalfChunk = 96;
+constexpr uint32_t kJit64HalfFlag = 1u << 19;
 
 // Stream width: columns per generated stream.  kJitNW (64) is the default;
 // narrower streams (32, 16, 8: same register contract, fewer accumulators,
@@ -157,6 +165,7 @@ struct JitImage {
     int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0, waves = kJitWaves;
     int tile_m = kJitTileM, chunk = kJitChunk;  // 64 / kJit64Chunk for the 64-row image
     int piece_rows = 0;                          // 64-row image: rows per DMA piece (16 or 8)
+    bool half = false;                           // 64-row image: the half ring (kJit64HalfChunk)
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
     std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
 };
@@ -165,14 +174,14 @@ struct JitImage {
 // rows64: the 64-row image (plain TCSC only; BaseTCSC order, VOP2 adds)
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                     const int32_t *rin, int K, int N, int B, JitImage &img, int nw = kJitNW,
-                    int waves = kJitWaves, bool far = false, bool rows64 = false);
+                    int waves = kJitWaves, bool far = false, bool rows64 = false, bool half = false);
 
 struct JitModule {
     void *module = nullptr;        // hipModule_t
     void *function = nullptr;      // hipFunction_t of tsg_jit_kernel
     void *probe = nullptr;         // hipFunction_t of tsg_jit_probe (region check, at load)
     std::string load(const std::vector<uint32_t> &code, int nw = kJitNW, int waves = kJitWaves,
-                     bool rows64 = false);  // "" on success
+                     bool rows64 = false, bool half = false);  // "" on success
     void unload();
 };
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
@@ -239,7 +248,8 @@ int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, vo
 int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int Kp, void *stream);
 // X [M][K] -> the blocked k-quad layout of the 64-row image (Mp % 64 == 0, Kp % 192 == 0;
 // piece_rows 16 or 8, kJit64R16Flag)
-int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream);
+int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream,
+                           int chunk = kJit64Chunk);
 int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,
                    const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                    int prelu, void *stream);

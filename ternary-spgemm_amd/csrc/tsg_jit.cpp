@@ -138,8 +138,8 @@ struct Emit {
 // 16), the code-prefetch sink, the DMA piece offsets, lane*128, and the
 // accumulators from the next even register.
 constexpr uint32_t kPairBytes = kJitTileM * 8;            // one k-row pair (64-row image: quad) of the tile in LDS: 1 KiB
-constexpr uint32_t kBufBytes = kJitChunk / 2 * kPairBytes; // one LDS chunk buffer (48 KiB)
 static_assert(kPairBytes == 1024, "one LDS-DMA piece (64 lanes x 16 B) is one pair row");
+static_assert(kJit64HalfChunk / 4 % 4 == 0, "half ring: whole pieces per wave at 4 waves");
 static_assert(kJit64TileM * 16 == (int)kPairBytes && kJit64Chunk / 4 == kJitChunk / 2,
               "64-row image: a quad row is one 1-KiB piece, 48 of them per chunk (the same ring)");
 constexpr uint32_t kXSlot0 = 8;                            // slot s: v[8 + 4s : 11 + 4s]
@@ -152,9 +152,9 @@ struct JitRegs {
     int pieces;         // DMA pieces (pair rows) per wave per chunk
     uint32_t lane128;   // v[lane * 128]
     uint32_t acc0;      // column c: v[acc0 + 2c : acc0 + 2c + 1]
-    explicit JitRegs(int waves)
-        : pieces(kJitChunk / 2 / waves), lane128(kDmaOffV + (uint32_t)(kJitChunk / 2 / waves)),
-          acc0((kDmaOffV + (uint32_t)(kJitChunk / 2 / waves) + 2) & ~1u)
+    explicit JitRegs(int waves, int units = kJitChunk / 2)  // units: 1-KiB pieces per chunk
+        : pieces(units / waves), lane128(kDmaOffV + (uint32_t)(units / waves)),
+          acc0((kDmaOffV + (uint32_t)(units / waves) + 2) & ~1u)
     {
     }
 };
@@ -243,20 +243,22 @@ int jit64_piece_rows()
 }
 
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
-                    int K, int N, int B, JitImage &img, int nw, int waves, bool far, bool r64)
+                    int K, int N, int B, JitImage &img, int nw, int waves, bool far, bool r64, bool half)
 {
     if (nw <= 0) nw = kJitNW;
     if (!jit_waves_ok(nw, waves)) waves = kJitWaves;
     if (B) r64 = false;  // BlockedTCSC: the 128-row image only
     if (nw > kJitNW && !r64) nw = kJitNW;  // 128 columns per wave: the 64-row image only (callers check)
+    if (!r64 || waves != 4) half = false;  // the half ring: 4-wave 64-row workgroups only
     if (r64) far = false;
     // K rows per chunk and per LDS unit (a pair, or a quad in the 64-row image):
     // 48 units of 1 KiB per chunk either way
-    const int CH = r64 ? kJit64Chunk : kJitChunk, U = r64 ? 4 : 2;
+    const int CH = r64 ? (half ? kJit64HalfChunk : kJit64Chunk) : kJitChunk, U = r64 ? 4 : 2;
+    const uint32_t kBuf = (uint32_t)(CH / U) * kPairBytes;  // one LDS ring buffer (48 KiB; half ring 24)
     // 64-row image: rows per DMA piece PR (16 or 8) and quads per piece 64 / PR
     // (tsg_internal.h, kJit64R16Flag)
     const int PR = r64 ? jit64_piece_rows() : 0, PQ = r64 ? 64 / PR : 0;
-    const JitRegs R(waves);
+    const JitRegs R(waves, CH / U);
     const int streams = waves;  // one stream per wave (no M split)
     const int kPieces = R.pieces;
     const uint32_t kLane128V = R.lane128, kAcc0 = R.acc0;
@@ -269,6 +271,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     img.tile_m = r64 ? kJit64TileM : kJitTileM;
     img.chunk = CH;
     img.piece_rows = PR;
+    img.half = half;
     img.Npad = ((N + tile_cols - 1) / tile_cols) * tile_cols;
     img.nch = std::max(1, (K + CH - 1) / CH);
     const int nch = img.nch, ntiles = img.Npad / tile_cols;
@@ -325,7 +328,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
                              (uint32_t)kJitRing | (r64 ? kJit64Format : kJitFormat) << 8 |
                                  (uint32_t)(m0k ? kJitM0kFlag : 0u) | (far ? kJitFarFlag : 0u) |
-                                 (PR == 16 ? kJit64R16Flag : 0u)});
+                                 (PR == 16 ? kJit64R16Flag : 0u) | (half ? kJit64HalfFlag : 0u)});
     const char *na = knob_value("TSG_JIT_NOALIGN");
     Emit E{code, !(na && na[0] == '1')};
     // TSG_JIT_CP="dma,touch": cache-policy bits of the LDS-DMA pieces and the
@@ -425,7 +428,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             return;
         const uint32_t sub = m0k ? (uint32_t)(i & 3) : 0u;
         if (sub == 0) {
-            E.m0_wave((uint32_t)(q % kJitRing) * kBufBytes + (uint32_t)i * kPairBytes);
+            E.m0_wave((uint32_t)(q % kJitRing) * kBuf + (uint32_t)i * kPairBytes);
             E.nop(0);  // M0 -> LDS-DMA
         }
         E.glds_x4(kDmaOffV + (uint32_t)i, sub * kPairBytes);
@@ -627,10 +630,12 @@ namespace {
 // The dispatcher of a stream width: lib/tsg_jit.co (kJitNW columns per wave)
 // or lib/tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile);
 // 4-wave workgroups: lib/tsg_jit_w<nw>_4w.co (TSG_JIT_WAVES=4); the 64-row
-// image: lib/tsg_jit64_w<nw>[_4w].co (TSG_JIT_ROWS64=1).
-std::string template_path(int nw, int waves, bool r64)
+// image: lib/tsg_jit64_w<nw>[_4w].co (TSG_JIT_ROWS64=1), its half ring
+// lib/tsg_jit64h_w<nw>.co (4 waves, TSG_JIT_HALF=1).
+std::string template_path(int nw, int waves, bool r64, bool half)
 {
-    const std::string name = r64 ? "tsg_jit64_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co"
+    const std::string name = r64 && half ? "tsg_jit64h_w" + std::to_string(nw) + ".co"
+                             : r64 ? "tsg_jit64_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co"
                              : nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
                              : "tsg_jit_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co";
     if (const char *dir = knob_value("TSG_JIT_DIR")) return std::string(dir) + "/" + name;  // tests: rx fallback
@@ -645,9 +650,9 @@ std::string template_path(int nw, int waves, bool r64)
 
 }  // namespace
 
-std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves, bool r64)
+std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves, bool r64, bool half)
 {
-    const std::string path = template_path(nw, waves, r64);
+    const std::string path = template_path(nw, waves, r64, half);
     std::ifstream f(path, std::ios::binary);
     if (!f) return "cannot open jit template " + path;
     std::vector<unsigned char> img((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -795,9 +800,36 @@ extern "C" int tsg_jit_codegen_wv(const int32_t *csp, const int32_t *csn, const 
     return TSG_OK;
 }
 
+namespace {
+int codegen64(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
+              int width, int waves, bool half, uint32_t *code, int64_t code_cap, int64_t *code_len,
+              uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len);
+}
+
 extern "C" int tsg_jit_codegen64(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
                                  int K, int N, int width, int waves, uint32_t *code, int64_t code_cap,
                                  int64_t *code_len, uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
+{
+    return codegen64(csp, csn, rip, rin, K, N, width, waves, false, code, code_cap, code_len, wcode, wcode_cap,
+                     wcode_len);
+}
+
+extern "C" int tsg_jit_codegen64h(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                                  int K, int N, int width, uint32_t *code, int64_t code_cap, int64_t *code_len,
+                                  uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
+{
+    if (width >= tsg::kJitNW) {
+        g_tsg_host_err = "tsg_jit_codegen64h: the half ring runs widths 32, 16, 8 (4 waves)";
+        return TSG_ERR_ARG;
+    }
+    return codegen64(csp, csn, rip, rin, K, N, width, 4, true, code, code_cap, code_len, wcode, wcode_cap,
+                     wcode_len);
+}
+
+namespace {
+int codegen64(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
+              int width, int waves, bool half, uint32_t *code, int64_t code_cap, int64_t *code_len,
+              uint32_t *wcode, int64_t wcode_cap, int64_t *wcode_len)
 {
     if (!tsg::jit64_width_ok(width) || !tsg::jit_waves_ok(width, waves)) {
         g_tsg_host_err = "tsg_jit_codegen64: unsupported shape " + std::to_string(width) + " x " +
@@ -815,7 +847,7 @@ extern "C" int tsg_jit_codegen64(const int32_t *csp, const int32_t *csn, const i
         return TSG_ERR_ARG;
     }
     tsg::JitImage img;
-    tsg::build_jit_code(csp, csn, rip, rin, K, N, 0, img, width, waves, false, true);
+    tsg::build_jit_code(csp, csn, rip, rin, K, N, 0, img, width, waves, false, true, half);
     if (code_len) *code_len = (int64_t)img.code.size();
     if (wcode_len) *wcode_len = (int64_t)img.wcode.size();
     if ((code && code_cap < (int64_t)img.code.size()) || (wcode && wcode_cap < (int64_t)img.wcode.size())) {
@@ -826,6 +858,8 @@ extern "C" int tsg_jit_codegen64(const int32_t *csp, const int32_t *csn, const i
     if (wcode) std::memcpy(wcode, img.wcode.data(), img.wcode.size() * 4);
     return TSG_OK;
 }
+
+}  // namespace
 
 extern "C" int tsg_jit_codegen_far(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
                                    int K, int N, uint32_t *code, int64_t code_cap, int64_t *code_len, uint32_t *wcode,

@@ -64,24 +64,34 @@ namespace {
 #ifndef TSG_JIT_ROWS64
 #define TSG_JIT_ROWS64 0
 #endif
+// TSG_JIT_HALF=1 (64-row image, 4 waves; lib/tsg_jit64h_w<NW>.co): the half
+// ring -- 96-row chunks of 24 pieces, 3 x 24 KiB of LDS, two workgroups per
+// CU -- with the 8-wave register contract (6 pieces per wave)
+#ifndef TSG_JIT_HALF
+#define TSG_JIT_HALF 0
+#endif
 constexpr int kJWaves = TSG_JIT_WAVES;
 constexpr int kJNW = TSG_JIT_NW;
 constexpr bool kJRows64 = TSG_JIT_ROWS64 != 0;
+constexpr bool kJHalf = TSG_JIT_HALF != 0;
+static_assert(!kJHalf || (kJRows64 && TSG_JIT_WAVES == 4), "the half ring is a 4-wave 64-row image");
 static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8 || (kJRows64 && kJNW == 128), "stream width");
 static_assert(kJWaves == 8 || (kJWaves == 4 && kJNW < 64), "waves per workgroup");
 constexpr int kJTileM = kJRows64 ? 64 : 128;
 constexpr int kJRowsPerLane = kJTileM / 64;
 constexpr int kJTileCols = kJWaves * kJNW;
 constexpr int kJRing = 3;                            // LDS buffers in the X^T ring (tsg_internal.h)
-constexpr int kJChunk = kJRows64 ? 192 : 96;         // K rows per chunk = 48 k-row quads / pairs
+constexpr int kJChunk = kJRows64 ? (kJHalf ? 96 : 192) : 96;  // K rows per chunk = 48 (half ring 24) quads / pairs
 constexpr int kJUnits = kJRows64 ? kJChunk / 4 : kJChunk / 2;  // 1-KiB LDS units per chunk
 constexpr int kJBufBytes = kJChunk * kJTileM * 4;    // 48 KiB
 constexpr int kJPieces = kJUnits / kJWaves;          // LDS-DMA pieces (1-KiB unit rows) per wave per chunk
 static_assert(kJBufBytes == kJUnits * 1024, "one LDS-DMA piece per unit row");
+static_assert(kJPieces == 6 || (kJWaves == 4 && kJPieces == 12), "register contract: 6 pieces (v108-113) or 12");
 constexpr uint32_t kJMagic0 = 0x7453474a, kJMagic1 = 0x314a4954;  // region header
 constexpr uint32_t kJM0kFlag = 1u << 16;  // header word 7: piece offsets in the DMA instruction (tsg_internal.h)
 constexpr uint32_t kJFormat = kJRows64 ? 3u : 2u;  // header word 7 bits 8-15: the X^T layout the code expects
 constexpr uint32_t kJR16Flag = 1u << 18;            // header word 7: 64-row image pieces of 16 rows x 4 quads
+constexpr uint32_t kJHalfFlag = 1u << 19;           // header word 7: the half ring
 #if TSG_JIT_ROWS64
 #define TSG_JIT_KERNEL_NAME tsg_jit64_kernel
 #else
@@ -92,7 +102,7 @@ typedef float F32x32 __attribute__((ext_vector_type(32)));
 typedef float F32x16 __attribute__((ext_vector_type(16)));
 typedef float F32x8 __attribute__((ext_vector_type(8)));
 
-#if TSG_JIT_WAVES == 8
+#if TSG_JIT_WAVES == 8 || TSG_JIT_HALF  // 6 DMA pieces per wave
 #define TSG_JIT_IN                                                                                  \
     "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),             \
         "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
@@ -139,7 +149,8 @@ extern "C" __global__ __launch_bounds__(64) void tsg_jit_probe(uint32_t *__restr
     }
 }
 
-extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
+// (the half ring: two workgroups per CU, so at most 256 VGPRs -- two waves per SIMD)
+extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_JIT_KERNEL_NAME(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
@@ -163,7 +174,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
                  : "scc");
     // never jump into a region that is not ours (or laid out for the other image)
     const uint32_t *hdr = reinterpret_cast<const uint32_t *>(base);
-    if (hdr[0] != kJMagic0 || hdr[1] != kJMagic1 || ((hdr[7] >> 8) & 0xffu) != kJFormat) {
+    if (hdr[0] != kJMagic0 || hdr[1] != kJMagic1 || ((hdr[7] >> 8) & 0xffu) != kJFormat ||
+        ((hdr[7] & kJHalfFlag) != 0) != kJHalf) {
         if (blockIdx.x == 0 && tid == 0) status[0] = 1u;
         return;
     }
@@ -240,8 +252,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64) void TSG_JIT_KERNEL_NAME(
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(xbase), "{s82}"(stride), "{s83}"(wb), \
                    TSG_JIT_IN                                                                       \
                  : TSG_JIT_CLOBBERS)
-#if TSG_JIT_ROWS64  // one accumulator VGPR per column (acc0 = v116; 4 waves: v122)
-#if TSG_JIT_WAVES == 8
+#if TSG_JIT_ROWS64  // one accumulator VGPR per column (acc0 = v116; 4 waves: v122, half ring v116)
+#if TSG_JIT_WAVES == 8 || TSG_JIT_HALF
 #define TSG_JIT_A0 "v[116:147]"
 #define TSG_JIT_A1 "v[148:179]"
 #define TSG_JIT_A16 "v[116:131]"

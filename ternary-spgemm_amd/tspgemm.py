@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
     "tcsc_hip_host_register", "tcsc_hip_host_unregister", "tcsc_hip_set_far", "tcsc_hip_call_far",
     "tsg_jit_codegen_far", "tsg_call_plan", "tsg_knob_check", "tcsc_hip_set_tile_rows", "tcsc_hip_call_tile_rows",
-    "tsg_jit_codegen64",
+    "tsg_jit_codegen64", "tsg_jit_codegen64h",
 )
 
 
@@ -135,6 +135,8 @@ def lib() -> C.CDLL:
     L.tcsc_hip_call_tile_rows.argtypes = [H, C.c_int]
     L.tsg_jit_codegen64.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                     C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
+    L.tsg_jit_codegen64h.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
+                                     C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tsg_call_plan.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int] + [C.POINTER(C.c_int)] * 7
     L.tcsc_hip_call_far.argtypes = [H, C.c_int]
     L.tsg_jit_codegen_far.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
@@ -276,18 +278,26 @@ def jit_codegen(csp, csn, rip, rin, K: int, N: int, B: int = 0, width: int = 64,
     return code, wcode
 
 
-def jit_codegen64(csp, csn, rip, rin, K: int, N: int, width: int = 16, waves: int = 4):
+def jit_codegen64(csp, csn, rip, rin, K: int, N: int, width: int = 16, waves: int = 4, half: bool = False):
     """Host-side machine code of the 64-row image (one M row per lane, VOP2
-    adds, k-quad X^T; include/ternary_spgemm_test.h tsg_jit_codegen64)."""
+    adds, k-quad X^T; include/ternary_spgemm_test.h tsg_jit_codegen64); half:
+    its half ring (4 waves, 96-row chunks; tsg_jit_codegen64h)."""
     csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
     nc, nw = C.c_int64(), C.c_int64()
     L = lib()
-    _check(L.tsg_jit_codegen64(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, width, waves, None, 0, C.byref(nc),
-                               None, 0, C.byref(nw)), "tsg_jit_codegen64")
+
+    def gen(code, cap_c, wcode, cap_w):
+        if half:
+            if waves != 4:
+                raise TSGError(-1, "tsg_jit_codegen64h", "the half ring runs 4-wave workgroups")
+            return L.tsg_jit_codegen64h(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, width, code, cap_c,
+                                        C.byref(nc), wcode, cap_w, C.byref(nw))
+        return L.tsg_jit_codegen64(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, width, waves, code, cap_c,
+                                   C.byref(nc), wcode, cap_w, C.byref(nw))
+    _check(gen(None, 0, None, 0), "tsg_jit_codegen64")
     code = np.empty(nc.value, np.uint32)
     wcode = np.empty(nw.value, np.uint32)
-    _check(L.tsg_jit_codegen64(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, width, waves, _ptr(code), nc.value,
-                               C.byref(nc), _ptr(wcode), nw.value, C.byref(nw)), "tsg_jit_codegen64")
+    _check(gen(_ptr(code), nc.value, _ptr(wcode), nw.value), "tsg_jit_codegen64")
     return code, wcode
 
 

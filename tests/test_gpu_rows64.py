@@ -157,3 +157,29 @@ def test_rows64_direct_x_and_staged(tsg, oracle_mod, monkeypatch, M, K, qblock):
         torch.cuda.synchronize()
         assert _bits_eq(Y.cpu().numpy(), ref), (M, K, shift)
     h.close()
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 4096, 16384), (37, 1000, 4096), (1, 777, 2048), (130, 1000, 2048),
+                                   (64, 96, 1500), (70, 97, 3000)])
+def test_rows64_half_ring(tsg, oracle_mod, monkeypatch, M, K, N):
+    """The half ring (TSG_JIT_HALF=1: the 4-wave shapes run 96-row chunks in a
+    72-KiB ring, two workgroups per CU; tsg_internal.h kJit64HalfChunk),
+    staged and direct X, bit for bit against the oracle."""
+    import torch
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, M + K + N))
+    b = np.linspace(-2, 2, N).astype(np.float32)
+    Xh = O.init_x_frac(M, K, 23)
+    ref = O.base_tcsc(Xh, t, b)
+    monkeypatch.setenv("TSG_JIT_HALF", "1")
+    h = _handle(tsg, t, K, N)
+    if h.jit_waves(M) != 4:
+        h.set_jit_width(16)
+    X = torch.from_numpy(Xh).cuda()
+    bt = torch.from_numpy(b).cuda()
+    for direct in ("0", "1"):
+        monkeypatch.setenv("TSG_JIT_XDIRECT", direct)
+        Y = h.gemm_torch(X, bt)
+        torch.cuda.synchronize()
+        assert _bits_eq(Y.cpu().numpy(), ref), (M, K, N, direct, h.jit_width(M), h.jit_waves(M))
+    h.close()

@@ -44,7 +44,10 @@ class Geom:
         # DMA pieces take their in-group offset from the instruction offset (one
         # M0 per 4 pieces; the dispatcher subtracts it from the global offsets)
         self.m0k = (int(code[7]) >> 16) & 1
-        assert int(code[7]) >> 19 == 0 and (self.r64 or (int(code[7]) >> 18) & 1 == 0)  # 16 m0k, 17 far, 18 R16
+        # 16 m0k, 17 far, 18 R16, 19 the half ring (64-row image, 4 waves, 96-row chunks)
+        assert int(code[7]) >> 20 == 0 and (self.r64 or (int(code[7]) >> 18) & 3 == 0)
+        self.half = (int(code[7]) >> 19) & 1
+        assert not self.half or (self.waves == 4 and self.chunk == 96)
         self.unit = 4 if self.r64 else 2              # k rows per LDS unit (quad / pair)
         self.pairs = self.chunk // self.unit          # units per chunk
         self.pair_bytes = self.tile_m * 4 * self.unit  # one unit row of the tile in LDS: 1 KiB
@@ -329,11 +332,12 @@ def emulate(code, wcode, X, K, N):
     return Y[:M, :N]
 
 
-def _check(tsg, O, M, K, N, s, seed, frac, W=None, width=64, waves=8, rows64=False):
+def _check(tsg, O, M, K, N, s, seed, frac, W=None, width=64, waves=8, rows64=False, half=False):
     W = O.gen_ternary(K, N, s, seed) if W is None else W
     t = O.tcsc_encode(W)
     if rows64:
-        code, wcode = tsg.jit_codegen64(*t.arrays, K, N, width=width, waves=waves)
+        code, wcode = tsg.jit_codegen64(*t.arrays, K, N, width=width, waves=waves, half=half)
+        assert Geom(code).half == half
         assert Geom(code).r64 and Geom(code).tile_m == 64
     else:
         code, wcode = tsg.jit_codegen(*t.arrays, K, N, width=width, waves=waves)
@@ -424,6 +428,21 @@ def test_jit_code_64row_image(tsg, oracle_mod, M, K, N, s, width, waves):
 @pytest.mark.parametrize("width,waves", [(32, 4), (16, 8), (8, 4)])
 def test_jit_code_64row_other_shapes(tsg, oracle_mod, width, waves):
     _check(tsg, oracle_mod, 70, 500, 300, 4, 99, True, width=width, waves=waves, rows64=True)
+
+
+@pytest.mark.parametrize("M,K,N,s", [(1, 1, 1, 1), (5, 70, 33, 2), (64, 200, 130, 4), (17, 300, 64, 8),
+                                     (3, 97, 9, 16), (100, 390, 40, 4), (70, 96, 50, 4), (70, 97, 50, 4)])
+@pytest.mark.parametrize("width", [32, 16, 8])
+def test_jit_code_64row_half_ring(tsg, oracle_mod, M, K, N, s, width):
+    """The half ring (96-row chunks of 24 pieces, 4 waves with the 8-wave
+    register contract; tsg_internal.h kJit64HalfChunk): emulated, bit for bit
+    against the oracle, K on and across chunk boundaries."""
+    for frac in (False, True):
+        _check(tsg, oracle_mod, M, K, N, s, 7 + K + N + width, frac, width=width, waves=4, rows64=True, half=True)
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(K, N, s, 1))
+    with pytest.raises(tsg.TSGError):
+        tsg.jit_codegen64(*t.arrays, K, N, width=64, waves=4, half=True)
 
 
 def test_jit_code_64row_dense_and_empty_columns(tsg, oracle_mod):
