@@ -173,8 +173,7 @@ def test_rows64_half_ring(tsg, oracle_mod, monkeypatch, M, K, N):
     ref = O.base_tcsc(Xh, t, b)
     monkeypatch.setenv("TSG_JIT_HALF", "1")
     h = _handle(tsg, t, K, N)
-    if h.jit_waves(M) != 4:
-        h.set_jit_width(16)
+    assert h.jit_waves(M) == 4, (M, K, N, h.jit_width(M))  # these shapes pick 4-wave workgroups
     X = torch.from_numpy(Xh).cuda()
     bt = torch.from_numpy(b).cuda()
     for direct in ("0", "1"):
