@@ -548,7 +548,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
         }
 #endif
     DeviceGuard g(h->device);
-    const std::string err = v.mod.load(img.code, nw, waves, r64);
+    const std::string err = v.mod.load(img.code, nw, waves, r64, half);
     if (!err.empty()) return fail(TSG_ERR_HIP, "jit kernel (width " + std::to_string(nw) + "): " + err);
     const size_t wb = img.wcode.size() * sizeof(uint32_t);
     if (hipMalloc(&v.d_wcode, std::max<size_t>(wb, 4)) != hipSuccess) {

@@ -143,7 +143,10 @@ extern "C" __global__ __launch_bounds__(64) void tsg_jit_probe(uint32_t *__restr
                  : "scc");
     const uint32_t *hdr = reinterpret_cast<const uint32_t *>(base);
     if (threadIdx.x == 0) {
-        const bool ok = hdr[0] == kJMagic0 && hdr[1] == kJMagic1;
+        // the region is ours and laid out for this dispatcher (the kernel makes
+        // the same check per launch, where a mismatch could only zero-exit)
+        const bool ok = hdr[0] == kJMagic0 && hdr[1] == kJMagic1 && ((hdr[7] >> 8) & 0xffu) == kJFormat &&
+                        ((hdr[7] & kJHalfFlag) != 0) == kJHalf;
         status[0] = ok ? 0u : 1u;
         status[1] = ok ? kJMagic0 : 0u;
     }
