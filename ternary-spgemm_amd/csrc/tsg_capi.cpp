@@ -126,6 +126,7 @@ constexpr int64_t kJitOneRoundWgs = 256;  // one jit workgroup per CU (144 KiB o
 constexpr double kFarXtBytes = 768.0 * 1024 * 1024;  // X^T >= 3x the 256 MiB Infinity Cache
 constexpr double kFarCodeBytes = 160.0 * 1024 * 1024;  // code image well inside it
 constexpr double kFarKeepXtBytes = 2048.0 * 1024 * 1024;  // X^T >= 8x it: the far image beats the 64-row one
+constexpr double kXDirectMinAddsPerRow = 32.0;  // 64-row image: direct X from width x density >= this
 constexpr int64_t kEllStarvedWgs = 64;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
 
@@ -292,20 +293,30 @@ bool far_xt(const tsg_tcsc *h, int M)
 // 1024 / PR contiguous bytes each; tsg_internal.h) when rows start 16-B
 // aligned (X 16-B aligned, K % 4 == 0), no piece straddles K (K % (256 / PR)
 // == 0: pieces at or past K are omitted, so nothing reads past a row's end)
-// and the per-lane offsets fit 32 bits -- on request only (TSG_JIT_XDIRECT=1,
-// read per call): every workgroup of an M tile gathers the same rows, 4K
-// bytes apart, chunk after chunk, and the kernel loses more than the X^T pass
-// costs at every M measured (profiles/r04f_shape_ab.jsonl,
-// r04g_bound_ab.jsonl; kernel / step us, K = 4096, N = 16384: M = 64
-// 85.2-85.7 / 91.6-92.4 direct vs 65.5-65.9 / 78.9-79.5 staged, either piece
-// shape; M = 512 208-209 / 215 vs 202-205 / 217-220; N = 4096: M = 256
-// 81.3 / 87.7 vs 56.7 / 71.1, M = 512 100.8 / 107.0-107.3 vs 92.0-92.6 /
-// 107.5-108.3).
-bool x_direct(const float *dX, int M, int K, int piece_rows)
+// and the per-lane offsets fit 32 bits.  Every workgroup of an M tile then
+// gathers the same rows, 4K bytes apart, chunk after chunk: that costs more
+// than the X^T pass unless a step's work is long enough to hide it -- so
+// automatic only for streams of >= 32 adds per k row per wave (width x
+// density: 128 columns at s <= 4, 64 at s <= 2).  Measured (kernel / step
+// us): configs[2] on 128 x 8 1231.4 / 1239.4 direct vs 1230.4 / 1273.0 staged
+// (profiles/r04z_direct_big_ab.jsonl); but s = 16 on 128 x 8 530.7 / 539.5 vs
+// 463.3 / 505.8, configs[1] on 16 x 8 94.3 / 101.0 vs 68.5 / 84.3, and K =
+// 4096, N = 16384: M = 64 (16 x 4) 85.2-85.7 / 91.6-92.4 vs 65.5-65.9 /
+// 78.9-79.5, M = 512 (64 x 8, s = 4) 208-209 / 215 vs 202-205 / 217-220
+// (r04f_shape_ab.jsonl, r04g_bound_ab.jsonl).  TSG_JIT_XDIRECT=1 / 0 forces it
+// on (where possible) / off, read per call (A/B).
+bool x_direct_auto(const tsg_tcsc *h, int nw)
+{
+    const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
+    return (double)nw * density >= kXDirectMinAddsPerRow;
+}
+
+bool x_direct(const tsg_tcsc *h, const float *dX, int M, int K, const tsg_tcsc::JitVariant &jv)
 {
     const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
-    const bool on = e && e[0] == '1';
-    return on && K > 0 && piece_rows > 0 && K % (256 / piece_rows) == 0 && ((uintptr_t)dX & 15) == 0 &&
+    const bool on = e ? e[0] == '1' : x_direct_auto(h, jv.nw);
+    const int pr = jv.piece_rows;
+    return on && K > 0 && pr > 0 && K % (256 / pr) == 0 && ((uintptr_t)dX & 15) == 0 &&
            (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
 }
 
@@ -359,14 +370,18 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     if (h->K >= 8192 && density > 0.375) return false;
     // 128 columns per wave fill whole rounds: twice the adds per staged chunk
     // and per X read of either 64-wide stream (profiles/r04l_w128_ab.jsonl,
-    // r04m_w128_big.jsonl) -- for sparse W or long K.  Dense W over short K
-    // depends on the data (r04o_xdata_ab.jsonl, kernel us): with bench.py's
-    // small-integer X the 128-row image is faster at configs[2] (1197 vs
-    // 1232), with full-mantissa X slower (1277 vs 1252) -- v_pk_add_f32 runs
-    // slower on high-entropy data, the VOP2 stream hardly -- so the 128-row
-    // image keeps it; the sparse end is the 64-row image's either way (s = 16:
-    // 468 vs 569 int, 496 vs 600 frac).
-    if ((density <= 0.1875 || h->K >= 8192) && pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW) return true;
+    // r04m_w128_big.jsonl) -- for sparse W or long K, and for dense W over
+    // short K when its stream reads X directly (x_direct): there the kernels
+    // depend on the data (r04o_xdata_ab.jsonl, kernel us: with bench.py's
+    // small-integer X the 128-row image runs configs[2] in 1197 vs 1232, with
+    // full-mantissa X 1277 vs 1252 -- v_pk_add_f32 slows on high-entropy data,
+    // the VOP2 stream hardly), and the 64-row image's step saves the X^T pass:
+    // configs[2] 1239.4 vs 1248.8 us per step with integer X
+    // (r04z_direct_big_ab.jsonl); the sparse end is the 64-row image's either
+    // way (s = 16: 468 vs 569 int, 496 vs 600 frac).
+    const bool direct_capable = h->K % (256 / tsg::jit64_piece_rows()) == 0 && x_direct_auto(h, tsg::kJit64WideNW);
+    if ((density <= 0.1875 || h->K >= 8192 || direct_capable) && pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW)
+        return true;
     if (s.nw != tsg::kJitNW || s.waves != tsg::kJitWaves) return true;
     const int64_t wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                         ((h->N + (int64_t)s.waves * s.nw - 1) / ((int64_t)s.waves * s.nw));
@@ -790,7 +805,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     // the 64-row image stages straight from row-major X (no X^T pass, no work
     // buffer) when every row starts 16-B aligned and the offsets fit 32 bits
-    const bool direct = r64 && x_direct(dX, M, K, jv->piece_rows);
+    const bool direct = r64 && x_direct(h, dX, M, K, *jv);
     if (!direct) {
         rc = ensure_work(h, M, capturing, r64, half);
         if (rc) return rc;

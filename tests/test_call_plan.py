@@ -7,10 +7,11 @@ import pytest
 
 
 @pytest.mark.parametrize("shape,plan", [
-    # configs[2] (the bench): 64 x 8, CU pairs on one code stream (2 x 16); the 128-row image
-    # with bench.py's integer X (1197 vs 1232 us for the 64-row 128 x 8; with full-mantissa X
-    # 1277 vs 1252, r04o_xdata_ab.jsonl)
-    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(2, 16), tmask=0)),
+    # configs[2] (the bench): the 64-row image's 128 x 8 reading X directly (no X^T pass), CU
+    # pairs on one code stream (2 x 16): step 1.2357-1.2368 vs 1.236-1.238 ms for the 128-row
+    # 64 x 8 with bench.py's integer X (r04z_bench_ab_images.jsonl), 1308 vs 1375 us with
+    # full-mantissa X (r04z_direct_big_ab.jsonl)
+    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=0)),
     # configs[1]: the 64-row image, 16 x 8 one-round grid (two waves per SIMD), code touches
     # thinned (round 4, r04j_waves_ab.jsonl: kernel / step 79.6 / 95.5 us vs 32 x 4 92.8 / 108.4;
     # the 128-row image's 16 x 4 96.8-100.3 / 111.8-115.9, r04g)
@@ -44,9 +45,9 @@ import pytest
     ((640, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 10), tmask=3)),
     ((1024, 4096, 4096, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(2, 16), tmask=3)),
     ((1024, 4096, 1024, 4), dict(kernel="tsg_jit64_kernel", width=16, waves=4, far=False, map=(2, 16), tmask=3)),
-    # ... the 128-row image where 64 x 8 fills whole rounds and W is dense over short K (M = 1024
-    # 339 vs 358 us, r04h; the 64-row 128 x 8 ties: 342 vs 338 int, 355 vs 356 frac, r04o)
-    ((1024, 4096, 16384, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(4, 8), tmask=3)),
+    # ... and 128 x 8 with direct X where W is dense over short K (M = 1024: kernels tie, 342 vs
+    # 338 us int, 355 vs 356 frac, r04o; the step drops the X^T pass)
+    ((1024, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=3)),
 ])
 def test_plan_matches_measured_winners(tsg, shape, plan):
     M, K, N, s = shape
@@ -63,7 +64,8 @@ def test_plan_matches_measured_winners(tsg, shape, plan):
     (96, 4096, 16384, "tsg_jit64_kernel"),
     (512, 4096, 16384, "tsg_jit64_kernel"),
     (1536, 4096, 16384, "tsg_jit64_kernel"),      # 128-row 64 x 8 in 1.5 rounds (547 vs 617 us, r04h)
-    (2048, 4096, 16384, "tsg_jit_kernel"),        # dense, short K, whole rounds (615 vs 617 us int, r04o)
+    (2048, 4096, 16384, "tsg_jit64_kernel"),      # dense, short K: 128 x 8, direct X (kernels 615 vs 617 us int, r04o)
+    (4096, 4100, 16384, "tsg_jit_kernel"),        # ... K % 16 != 0: no direct X, the 128-row image
     (32, 1024, 4096, "tsg_tcsc_ell_kernel"),      # configs[0]
     (16, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 16 (184 vs 247 us, r04g)
     (17, 16384, 16384, "tsg_jit64_kernel"),       # (M = 32: 310 vs 248 us)

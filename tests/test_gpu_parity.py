@@ -140,15 +140,15 @@ def test_far_image_vs_oracle(tsg, oracle_mod):
 
 
 def test_auto_width_small_m(tsg, oracle_mod):
-    """Automatic width: narrow streams for small M, the 128-row image's 64 at
-    config 3's M; one handle switching widths and images call by call stays
-    bit-exact."""
+    """Automatic width: narrow streams for small M, 128 columns per wave (the
+    64-row image) at config 3's M; one handle switching widths and images
+    call by call stays bit-exact."""
     O = oracle_mod
     K, N = 1024, 4096
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, 77))
     h = tsg.TCSCDevice(*t.arrays, K, N)
     h.set_small_m(1)
-    assert h.jit_width(32) < 64 and h.jit_width(8192) == 64 and h.call_kernel(8192) == "tsg_jit_kernel"
+    assert h.jit_width(32) < 64 and h.jit_width(8192) == 128 and h.call_kernel(8192) == "tsg_jit64_kernel"
     b = np.full(N, 2.0, np.float32)
     for M in (32, 8192, 7):
         X = O.init_x_frac(M, K, M)

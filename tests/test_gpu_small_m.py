@@ -89,7 +89,7 @@ def test_auto_choice_and_structural_edges(tsg, oracle_mod):
     O = oracle_mod
     t = O.tcsc_encode(O.gen_ternary(1024, 4096, 4, 77))
     h = tsg.TCSCDevice(*t.arrays, 1024, 4096)
-    assert h.call_kernel(1) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(4096) == "tsg_jit_kernel"
+    assert h.call_kernel(1) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(4096) == "tsg_jit64_kernel"
     assert h.call_kernel(4) == "tsg_tcsc_ell_pc_kernel" and h.call_kernel(5) == "tsg_tcsc_ell_kernel"
     h.set_small_m(1)
     assert h.call_kernel(1) == "tsg_jit64_kernel"  # small M off: the 64-row weight-compiled image
