@@ -134,9 +134,8 @@ int tsg_ell_build(const int32_t *col_start_pos, const int32_t *col_start_neg, co
  * (default), 64 = the 64-row image, 128 = the 128-row image (v_pk_add_f32) for
  * every weight-compiled call (plain TCSC only).  tcsc_hip_call_tile_rows: the
  * M tile (64 / 128) of a call with M rows, 0 if it runs a small-M walk.
- * Which image is faster can depend on X itself: with
- * full-mantissa activations, dense W and large M, 64 can beat the automatic
- * choice by a few percent. */
+ * (The 128-row image's v_pk_add_f32 stream slows on full-mantissa X more than
+ * the 64-row image's VOP2 stream) */
 int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows);
 int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M);
 
