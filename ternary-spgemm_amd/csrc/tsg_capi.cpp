@@ -496,13 +496,18 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
 // (configs[2] +4%, s = 16 +15%), and with 2 M tiles per stream it loses too
 // ((256, 4096, 16384) +7-17%, r03g_ref_cases.jsonl), so every tile touches.
 // TSG_JIT_GN / TSG_JIT_GM / TSG_JIT_TMASK override (A/B).
-void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, int &tmask)
+void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, int &tmask, int nw = 0)
 {
     static const int env_gn = [] { const char *e = tsg::knob_value("TSG_JIT_GN"); return e ? atoi(e) : 0; }();
     static const int env_gm = [] { const char *e = tsg::knob_value("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
     static const int env_tm = [] { const char *e = tsg::knob_value("TSG_JIT_TMASK"); return e ? atoi(e) : -1; }();
-    tmask = env_tm >= 0 ? env_tm : ((int64_t)mtiles * ntiles <= kJitOneRoundWgs && mtiles >= 4 ? 3 : 0);
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
+    // the 64-row image's 128-wide streams over dense W and short K thin their
+    // touches over several rounds too: configs[2] 1.2243-1.2252 vs 1.2315-1.2317 ms kernel,
+    // three alternating bench runs each (profiles/r04t_tmask_bench_ab.txt)
+    const bool wide_dense = nw == tsg::kJit64WideNW && density > 0.1875 && h->K < 8192;
+    tmask = env_tm >= 0 ? env_tm
+                        : (((int64_t)mtiles * ntiles <= kJitOneRoundWgs || wide_dense) && mtiles >= 4 ? 3 : 0);
     int n = 2, m = 16;
     // s = 8 over long K takes the long-stream map ((64000, 16384, 4096) s = 8:
     // 13.72-13.73 ms vs 15.3-15.8 at 4 x 8, profiles/r03f_sparse_big_ab.txt);
@@ -833,7 +838,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     int gn = 2, gm = 16, tmask = 0;
     if (h->kind == tsg_tcsc::kJit)
-        pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask);
+        pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask, r64 ? jv->nw : 0);
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                jv->nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
@@ -1478,7 +1483,7 @@ extern "C" int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int 
         *width = sh.nw;
         *waves = sh.waves;
         *far = sh.far ? 1 : 0;
-        pick_jit_map(&h, (M + tm - 1) / tm, ntiles, *gn, *gm, *tmask);
+        pick_jit_map(&h, (M + tm - 1) / tm, ntiles, *gn, *gm, *tmask, r64 ? sh.nw : 0);
     }
     return TSG_OK;
 }

@@ -10,8 +10,9 @@ import pytest
     # configs[2] (the bench): the 64-row image's 128 x 8 reading X directly (no X^T pass), CU
     # pairs on one code stream (2 x 16): step 1.2357-1.2368 vs 1.236-1.238 ms for the 128-row
     # 64 x 8 with bench.py's integer X (r04z_bench_ab_images.jsonl), 1308 vs 1375 us with
-    # full-mantissa X (r04z_direct_big_ab.jsonl)
-    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=0)),
+    # full-mantissa X (r04z_direct_big_ab.jsonl); code touches thinned (1.2243-1.2252 vs
+    # 1.2315-1.2317 ms kernel, r04t_tmask_bench_ab.txt)
+    ((4096, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 16), tmask=3)),
     # configs[1]: the 64-row image, 16 x 8 one-round grid (two waves per SIMD), code touches
     # thinned (round 4, r04j_waves_ab.jsonl: kernel / step 79.6 / 95.5 us vs 32 x 4 92.8 / 108.4;
     # the 128-row image's 16 x 4 96.8-100.3 / 111.8-115.9, r04g)
