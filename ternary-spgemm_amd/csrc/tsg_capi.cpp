@@ -502,12 +502,14 @@ void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, i
     static const int env_gm = [] { const char *e = tsg::knob_value("TSG_JIT_GM"); return e ? atoi(e) : 0; }();
     static const int env_tm = [] { const char *e = tsg::knob_value("TSG_JIT_TMASK"); return e ? atoi(e) : -1; }();
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
-    // the 64-row image's 128-wide streams over short K thin their touches over
-    // several rounds too: configs[2] 1.2243-1.2252 vs 1.2315-1.2317 ms kernel,
-    // three alternating bench runs each (profiles/r04t_tmask_bench_ab.txt);
-    // configs[3] s = 8 / 16 680.6-681.2 / 444.3-448.1 vs 684.7-690.5 /
-    // 458.2-462.8 us (r04t_tmask_sparse_ab.txt)
-    const bool wide_short = nw == tsg::kJit64WideNW && h->K < 8192;
+    // the 64-row image's 128-wide streams thin their touches over several
+    // rounds too: configs[2] 1.2243-1.2252 vs 1.2315-1.2317 ms kernel, three
+    // alternating bench runs each (profiles/r04t_tmask_bench_ab.txt); configs[3]
+    // s = 8 / 16 680.6-681.2 / 444.3-448.1 vs 684.7-690.5 / 458.2-462.8 us
+    // (r04t_tmask_sparse_ab.txt); (16000, 8192, 2048) s = 4 / 8 1227-1239 /
+    // 729-735 vs 1248-1261 / 739-749 us (r04t_tmask_long_ab.txt; (8192, 16384,
+    // 4096) within its run-to-run spread)
+    const bool wide_short = nw == tsg::kJit64WideNW;
     tmask = env_tm >= 0 ? env_tm
                         : (((int64_t)mtiles * ntiles <= kJitOneRoundWgs || wide_short) && mtiles >= 4 ? 3 : 0);
     int n = 2, m = 16;
