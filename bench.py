@@ -8,11 +8,13 @@ the TCSC kernel).  Workload at N=1 = BASELINE.json configs[2]
 (M=4096 K=4096 N=16384 s=4).
 
 Multi-GPU (one process per GPU, RCCL): W's columns are sharded
-(tsg_dist.py).  `value` is the compute step (every rank's Y column block, no
-collective on the compute path); for world > 1 the line also carries the
-RCCL all-gather of the Y blocks into the row-major [M, N] result:
-`allgather_ms` (the gather alone) and `with_allgather` (the step as
-compute + gather pipelined by M chunks, tsg_dist.GatherPipeline).
+(tsg_dist.py).  At world > 1 a step is configs[4]'s WHOLE work: every rank's
+Y column block computed AND the RCCL all-gather of the blocks into the
+row-major [M, N_total] result on every rank, pipelined by M chunks
+(tsg_dist.GatherPipeline) -- `value` and `ms_per_step` time exactly that.
+The compute-only step (no collective) is reported beside it as
+`compute_only`, the gather alone as `allgather_ms` with its achieved
+bandwidth per GPU (`allgather_gbps_per_gpu` = bytes received per GPU / time).
   * default (weak): every rank owns --N columns (N_total = N * P; P = 8 is
     configs[4], N = 131072); each rank draws only its own column block.
   * --strong: N_total = --N fixed, N/P columns per rank (same W for every P).
@@ -21,12 +23,14 @@ Launch: under torchrun (WORLD_SIZE set) this process is one rank, and
 WORLD_SIZE must equal --gpus.  Without WORLD_SIZE and with --gpus N > 1 this
 process is only the launcher: it starts N rank processes (RANK / LOCAL_RANK /
 WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT) before anything touches the
-GPU, forwards rank 0's JSON line, and exits non-zero if a rank fails or the
-world that ran differs from --gpus.  A rank whose LOCAL_RANK has no GPU fails
-(RCCL), except in the one-GPU rehearsal TSG_BENCH_BACKEND=gloo, where ranks
-share the visible devices.
+GPU, forwards rank 0's JSON line, and exits non-zero if a rank fails, if the
+world that ran differs from --gpus, or if the ranks are still running at the
+--timeout deadline (then they are stopped by PID and the launcher names
+them).  A rank whose LOCAL_RANK has no GPU fails (RCCL), except in the
+one-GPU rehearsal TSG_BENCH_BACKEND=gloo, where ranks share the visible
+devices.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong] [--timeout S]
 """
 from __future__ import annotations
 
@@ -70,6 +74,9 @@ def parse():
     ap.add_argument("--seed-x", type=int, default=12345)
     ap.add_argument("--cpu-rows", type=int, default=512,
                     help="rows of the bounded single-thread CPU-baseline samples (0 = skip the CPU legs)")
+    ap.add_argument("--timeout", type=float, default=420.0,
+                    help="launcher deadline in seconds (--gpus N > 1 without torchrun): ranks still running "
+                         "then are stopped by PID and the launcher exits 124")
     return ap.parse_args()
 
 
@@ -156,13 +163,17 @@ def launch_ranks(a) -> int:
     children (never an exec of this process).  Rank 0's stdout (the JSON
     line) is forwarded after checking its n_gpus; every other output goes to
     stderr.  If a rank fails, the others are terminated (by PID) and the
-    failing exit code is returned."""
+    failing exit code is returned.  If ranks are still running at the
+    deadline (--timeout: e.g. one stuck in the RCCL rendezvous, neither
+    exited nor failed), every running rank is terminated by PID, the
+    launcher names them and returns 124."""
     import subprocess
     import threading
     n = a.gpus
     port = _free_port()
     dry = os.environ.get("TSG_BENCH_DRYRUN") == "1"
     procs, outs = [], [[] for _ in range(n)]
+    t_launch = time.time()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -175,27 +186,42 @@ def launch_ranks(a) -> int:
             t = threading.Thread(target=lambda p=p, o=outs[r]: o.extend(p.stdout), daemon=True)
             t.start()
             readers.append(t)
+
+    def stop_running():
+        # SIGTERM, then SIGKILL after 10 s, by PID (never by pattern)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + 10
+        while time.time() < t_end and any(p.poll() is None for p in procs):
+            time.sleep(0.1)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+
     rc = 0
     while True:
         codes = [p.poll() for p in procs]  # every rank, every round (no short-circuit)
         bad = [c for c in codes if c not in (None, 0)]
         if bad:
             # a failed rank leaves the others waiting in the rendezvous or a
-            # collective: stop them (SIGTERM, then SIGKILL), by PID
+            # collective: stop them
             rc = bad[0]
             print(f"bench.py: a rank exited with {rc}; terminating the others", file=sys.stderr)
-            for p in procs:
-                if p.poll() is None:
-                    p.terminate()
-            t_end = time.time() + 10
-            while time.time() < t_end and any(p.poll() is None for p in procs):
-                time.sleep(0.1)
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()
+            stop_running()
             break
         if all(c is not None for c in codes):
             break
+        if time.time() - t_launch > a.timeout:
+            running = [r for r, c in enumerate(codes) if c is None]
+            print(f"bench.py: deadline of {a.timeout:g} s passed with rank(s) {running} still running "
+                  f"(pids {[procs[r].pid for r in running]}); terminating them", file=sys.stderr)
+            stop_running()
+            for t in readers:
+                t.join(timeout=5)
+            print(f"bench.py: no result: --gpus {n} timed out", file=sys.stderr)
+            return 124
         time.sleep(0.2)
     for t in readers:
         t.join(timeout=10)
@@ -227,6 +253,100 @@ def launch_ranks(a) -> int:
     return 0
 
 
+def headline(world: int, steps: int, flops_all: int, compute_elapsed_max: float, pipe_elapsed_max=None):
+    """(value GFLOP/s, ms_per_step) of the line.  At world > 1 a step is
+    configs[4]'s whole work: the compute of every rank's column block AND the
+    all-gather into row-major [M, N_total] (tsg_dist.GatherPipeline), timed
+    over exactly `steps` steps, max over ranks; the compute-only step is a
+    side figure.  At world == 1 there is no collective: the compute step."""
+    if world > 1:
+        if pipe_elapsed_max is None:
+            raise ValueError("world > 1: the headline is the compute + all-gather step; it was not measured")
+        el = pipe_elapsed_max
+    else:
+        el = compute_elapsed_max
+    return flops_all * steps / el / 1e9, el / steps * 1e3
+
+
+def build_line(a, *, world, mode, backend, M, K, Nr, Ntot, s, nnz, nnz_all, kname, compute_elapsed_max,
+               kern_ms_max, gather=None, traffic=None, cpu=None, e2e=None, stream_ms=None, setup_s=0.0,
+               clock_warmup=(0.0, 0)) -> dict:
+    """The JSON line rank 0 prints (bench.py contract), from the measured
+    quantities (max over ranks).  Pure: tests/test_bench_launch.py checks it
+    without a GPU."""
+    flops_all = M * (nnz_all + Ntot)  # sum over ranks of T.flops(M, Nr, nnz_rank)
+    value, ms_step = headline(world, a.steps, flops_all, compute_elapsed_max,
+                              None if gather is None else gather["pipeline_elapsed_s"])
+    alg_bytes = T.algorithmic_bytes(M, Nr, K, nnz)  # per launch, this rank
+    adds = T.flops(M, Nr, nnz)                       # per launch: one IEEE add per (m, nonzero) + bias
+    achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
+    binding_frac = round(adds / (kern_ms_max * 1e-3) / 1e12 / VALU_PEAK_TADDS, 4)
+    if world == 1:
+        workload = "BASELINE configs[2]" if (M, K, Nr, s) == (4096, 4096, 16384, 4) else "custom"
+    elif mode == "weak":
+        workload = (f"BASELINE configs[4]-style weak column shard + all-gather: {Nr} columns per GPU, "
+                    f"N_total={Ntot}" + (" (= configs[4])" if (M, K, Ntot, s, world) == (4096, 4096, 131072, 4, 8)
+                                         else ""))
+    else:
+        workload = f"strong column shard of N={Ntot} over {world} GPUs ({Nr} columns per GPU) + all-gather"
+    compute_only = {"ms_per_step": round(compute_elapsed_max / a.steps * 1e3, 4),
+                    "value": round(flops_all * a.steps / compute_elapsed_max / 1e9, 3), "unit": "GFLOP/s",
+                    "note": "every rank's Y column block, no collective"}
+    gather_info = None
+    if gather is not None:
+        coll = "RCCL" if backend == "nccl" else backend
+        gather_info = {"ms_per_step": round(ms_step, 4), "value": round(value, 3), "unit": "GFLOP/s",
+                       "note": f"the headline: compute + {coll} all-gather of Y into row-major [M, N_total], "
+                               f"pipelined by {gather['chunks']} M chunks (tsg_dist.GatherPipeline)",
+                       "columns_match_compute_only": gather["columns_match"],
+                       "every_block_delivered": gather.get("blocks_match"),
+                       "bytes_received_per_gpu": gather["bytes_received_per_gpu"]}
+    out = {
+        "metric": "effective GFLOP/s + achieved HBM GB/s (% roofline), TCSC spGEMM M×K×N at s",
+        "value": round(value, 3),
+        "unit": "GFLOP/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": mode,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (generateSparseMatrix law, seed_w=%d; X integer U[-512,512], seed_x=%d; b=2)"
+                % (a.seed_w, a.seed_x),
+        "config": {"workload": workload, "M": M, "K": K, "N_per_gpu": Nr, "N_total": Ntot, "s": s,
+                   "nnz_per_gpu": nnz, "parallelism": f"W columns x{world}"
+                   + (" + all-gather of Y" if world > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                     "traffic": traffic,
+                     "kernel": kname, "kernel_ms": round(kern_ms_max, 4),
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "kernel_gflops": round(adds / (kern_ms_max * 1e-3) / 1e9, 2),
+                     "traffic_source": (os.path.relpath(PROFILE_PMC, REPO) if traffic is not None else None),
+                     "binding": {"resource": "valu fp32 adds (DESIGN.md 4)", "adds_per_launch": adds,
+                                 "achieved_Tadds": round(adds / (kern_ms_max * 1e-3) / 1e12, 2),
+                                 "peak_Tadds": round(VALU_PEAK_TADDS, 2), "frac": binding_frac}},
+        # the roof that binds this kernel (DESIGN.md 4.1), top level so a
+        # parser that keeps only flat keys of `roofline` still sees it
+        "binding_roof": {"resource": "valu fp32 adds", "frac": binding_frac, "kernel": kname,
+                         "achieved_Tadds": round(adds / (kern_ms_max * 1e-3) / 1e12, 2),
+                         "peak_Tadds": round(VALU_PEAK_TADDS, 2)},
+        "cpu_baseline": cpu,
+        "compute_only": compute_only if world > 1 else None,
+        "stream_ms_per_step": None if stream_ms is None else round(stream_ms / a.steps, 4),
+        "e2e_host_pointers": e2e,
+        "allgather_ms": None if gather is None else round(gather["allgather_ms"], 3),
+        "allgather_gbps_per_gpu": (None if gather is None else
+                                   round(gather["bytes_received_per_gpu"] / (gather["allgather_ms"] * 1e-3) / 1e9, 2)),
+        "with_allgather": gather_info,
+        "setup_s": round(setup_s, 2),
+        "clock_warmup": {"seconds": round(clock_warmup[0], 3), "steps": clock_warmup[1]},
+    }
+    return out
+
+
 def main():
     a = parse()
     if launch_mode(a.gpus, os.environ) == "launch":
@@ -244,6 +364,10 @@ def main():
             if rank == int(os.environ["TSG_BENCH_DRYRUN_FAIL_RANK"]):
                 sys.exit(3)
             time.sleep(600)
+        if os.environ.get("TSG_BENCH_DRYRUN_HANG_RANK") is not None:
+            # one rank never exits nor fails (stuck in a rendezvous); the others finish
+            if rank == int(os.environ["TSG_BENCH_DRYRUN_HANG_RANK"]):
+                time.sleep(600)
         print(json.dumps({"rank": rank, "world": world, "local_rank": local,
                           "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
         return
@@ -327,8 +451,12 @@ def main():
     h.set_timing(False)
     stream_ms = ev0.elapsed_time(ev1)
 
-    # --- world > 1: the RCCL all-gather of the Y column blocks (north_star's
-    # collective), alone and pipelined with the compute by M chunks
+    # --- world > 1: configs[4]'s whole step = the compute of this rank's
+    # column block AND the RCCL all-gather of every rank's block into the
+    # row-major [M, N_total] Y (north_star's collective), pipelined by M
+    # chunks.  This is the headline at world > 1: exactly a.steps steps,
+    # barrier + synchronize on both sides, max over ranks.  The gather alone
+    # is timed first (allgather_ms, its bandwidth per GPU).
     gather = None
     if world > 1:
         Yfull = torch.empty((M, Ntot), device=dev)
@@ -362,13 +490,22 @@ def main():
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        pipe_s = (time.perf_counter() - tp) / a.steps
-        # the pipelined result equals the compute-only blocks (this rank's columns)
+        pipe_elapsed = time.perf_counter() - tp
+        # the pipelined Y: this rank's columns equal its compute-only block,
+        # and every other rank's columns carry that rank's block (a checksum
+        # of each block, all-gathered, against the same checksum of Y_full)
         ok = torch.equal(Yfull[:, n0:n1].view(torch.int32), Y.view(torch.int32))
-        tg = torch.tensor([ag_s, pipe_s, 0.0 if ok else 1.0], device=dev, dtype=torch.float64)
+        mine = Y.view(torch.int32).to(torch.int64).sum().reshape(1)
+        sums = torch.empty(world, dtype=torch.int64, device=dev)
+        D._all_gather_into(sums, mine)
+        got = torch.stack([Yfull[:, c0:c1].view(torch.int32).to(torch.int64).sum()
+                           for c0, c1 in (D.column_shard(Ntot, world, r) for r in range(world))])
+        blocks_ok = torch.equal(sums, got)
+        tg = torch.tensor([ag_s, pipe_elapsed, 0.0 if ok else 1.0, 0.0 if blocks_ok else 1.0],
+                          device=dev, dtype=torch.float64)
         dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-        gather = {"allgather_ms": float(tg[0]) * 1e3, "pipeline_ms": float(tg[1]) * 1e3,
-                  "columns_match": float(tg[2]) == 0.0,
+        gather = {"allgather_ms": float(tg[0]) * 1e3, "pipeline_elapsed_s": float(tg[1]),
+                  "columns_match": float(tg[2]) == 0.0, "blocks_match": float(tg[3]) == 0.0,
                   "bytes_received_per_gpu": 4 * M * (Ntot - Nr), "chunks": len(pipe.ranges)}
         del pipe, Yfull
 
@@ -421,12 +558,6 @@ def main():
         cpu = cpu_baseline(X, csp, csn, rip, rin, K, Nr, s, Y, a.cpu_rows)
 
     if rank == 0:
-        flops_all = M * (nnz_all + Ntot)  # sum over ranks of T.flops(M, Nr, nnz_rank)
-        value = flops_all * a.steps / elapsed_max / 1e9
-        ms_step = elapsed_max / a.steps * 1e3
-        alg_bytes = T.algorithmic_bytes(M, Nr, K, nnz)  # per launch, this rank
-        adds = T.flops(M, Nr, nnz)                       # per launch: one IEEE add per (m, nonzero) + bias
-        achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
         traffic = None
         try:
             # HBM bytes per launch of THIS kernel on THIS workload, from the
@@ -437,58 +568,10 @@ def main():
                 traffic = pm.get("kernels", {}).get(kname, {}).get("hbm_bytes")
         except Exception:
             pass
-        if world == 1:
-            workload = "BASELINE configs[2]" if (M, K, Nr, s) == (4096, 4096, 16384, 4) else "custom"
-        elif mode == "weak":
-            workload = (f"BASELINE configs[4]-style weak column shard: {Nr} columns per GPU, N_total={Ntot}"
-                        + (" (= configs[4])" if (M, K, Ntot, s, world) == (4096, 4096, 131072, 4, 8) else ""))
-        else:
-            workload = f"strong column shard of N={Ntot} over {world} GPUs ({Nr} columns per GPU)"
-        with_gather = None
-        if gather is not None:
-            with_gather = {"ms_per_step": round(gather["pipeline_ms"], 4),
-                           "value": round(flops_all / (gather["pipeline_ms"] * 1e-3) / 1e9, 3),
-                           "unit": "GFLOP/s",
-                           "note": f"compute + {'RCCL' if backend == 'nccl' else backend} all-gather of Y into "
-                                   f"row-major [M, N_total], pipelined by {gather['chunks']} M chunks "
-                                   "(tsg_dist.GatherPipeline)",
-                           "columns_match_compute_only": gather["columns_match"],
-                           "bytes_received_per_gpu": gather["bytes_received_per_gpu"]}
-        out = {
-            "metric": "effective GFLOP/s + achieved HBM GB/s (% roofline), TCSC spGEMM M×K×N at s",
-            "value": round(value, 3),
-            "unit": "GFLOP/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms_step, 4),
-            "higher_is_better": True,
-            "scaling": mode,
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (generateSparseMatrix law, seed_w=%d; X integer U[-512,512], seed_x=%d; b=2)"
-                    % (a.seed_w, a.seed_x),
-            "config": {"workload": workload, "M": M, "K": K, "N_per_gpu": Nr, "N_total": Ntot, "s": s,
-                       "nnz_per_gpu": nnz, "parallelism": f"W columns x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                         "traffic": traffic,
-                         "kernel": kname, "kernel_ms": round(kern_ms_max, 4),
-                         "algorithmic_bytes_per_launch": alg_bytes,
-                         "kernel_gflops": round(adds / (kern_ms_max * 1e-3) / 1e9, 2),
-                         "traffic_source": (os.path.relpath(PROFILE_PMC, REPO) if traffic is not None else None),
-                         "binding": {"resource": "valu fp32 adds (DESIGN.md 4)", "adds_per_launch": adds,
-                                     "achieved_Tadds": round(adds / (kern_ms_max * 1e-3) / 1e12, 2),
-                                     "peak_Tadds": round(VALU_PEAK_TADDS, 2),
-                                     "frac": round(adds / (kern_ms_max * 1e-3) / 1e12 / VALU_PEAK_TADDS, 4)}},
-            "cpu_baseline": cpu,
-            "stream_ms_per_step": round(stream_ms / a.steps, 4),
-            "e2e_host_pointers": e2e,
-            "allgather_ms": None if gather is None else round(gather["allgather_ms"], 3),
-            "with_allgather": with_gather,
-            "setup_s": round(setup_s, 2),
-            "clock_warmup": {"seconds": round(clock_warmup_s, 3), "steps": n_clock},
-        }
+        out = build_line(a, world=world, mode=mode, backend=backend, M=M, K=K, Nr=Nr, Ntot=Ntot, s=s, nnz=nnz,
+                         nnz_all=nnz_all, kname=kname, compute_elapsed_max=elapsed_max, kern_ms_max=kern_ms_max,
+                         gather=gather, traffic=traffic, cpu=cpu, e2e=e2e, stream_ms=stream_ms,
+                         setup_s=setup_s, clock_warmup=(clock_warmup_s, n_clock))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -180,8 +180,12 @@ int tcsc_hip_kernel_time(tsg_tcsc *h, double *total_ms, int64_t *launches, int r
 const char *tcsc_hip_kernel_name(const tsg_tcsc *h);
 
 /* The device kernel a call with M rows launches on this handle (calls pick
- * per M): "tsg_jit_kernel", "tsg_tcsc_ell_kernel" /
- * "tsg_tcsc_ell_pc_kernel" (the small-M walks) or "tsg_tcsc_rx_kernel". */
+ * per M): "tsg_jit64_kernel" (the weight-compiled 64-row image:
+ * one M row per lane; the default for M <= 512 and for configs[2]),
+ * "tsg_jit_kernel" (the weight-compiled 128-row image; also what a call runs
+ * after the image it picked could not be loaded -- logged on stderr),
+ * "tsg_tcsc_ell_kernel" / "tsg_tcsc_ell_pc_kernel" (the small-M walks) or
+ * "tsg_tcsc_rx_kernel". */
 const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M);
 
 const char *tcsc_hip_last_error(void);

@@ -12,6 +12,16 @@
 // is the reference's own (main.cpp:192-247): fresh Y, call, compare_results
 // against the dense GEMM, "Test case <name> passed!" or exit(1).
 //
+// With `-perf` (after the reference's argv) the reference's benchmark loop
+// follows (main.cpp:253-293): its own timing harness, cpp_impl/perf.cpp
+// compiled UNMODIFIED with -DCALIBRATE (the x86 rdtsc path, perf.cpp:37-71,
+// 298-339), times every registered comp_func -- "Running: / cycles / Speedup
+// is:" relative to "BaseTCSC" (main.cpp:10,259-263).  "BaseTCSC" and
+// "BaseTCSC_PreLU" are registered first, as main.cpp:76-81 registers them:
+// comp.h does not build here (<arm_neon.h>, comp.h:6), so they are the
+// oracle's restatements (oracle/tcsc_oracle.c, comp.h:25-69 and
+// comp_prelu.h:12-70) -- test infrastructure, never in the package.
+//
 // TEST INFRASTRUCTURE: built by `make -C oracle refplugin` into
 // oracle/_ref/plugin_ref_check (gitignored; travels to the GPU box like
 // libref.so).  tests/test_integration_ref.py builds it on the CPU (compile +
@@ -22,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iostream>
 #include <memory>
 #include <string>
 #include <thread>
@@ -29,9 +40,14 @@
 
 #include "common.h"
 #include "data_structures/DataStructureInterface.hpp"
+#include "perf.h"
 #include "sparseUtils.h"
 #define TSG_WITH_REFERENCE_DSI
 #include "tcsc_hip_plugin.hpp"
+
+extern "C" {
+#include "tcsc_oracle.h"
+}
 
 // the registry of main.cpp:12-33 (its definitions live in main.cpp, which has
 // its own main(); the declarations come from common.h:15-16)
@@ -71,6 +87,8 @@ int main(int argc, char **argv)
         N = std::atoi(argv[6]);
         s = std::atoi(argv[8]);
     }
+    bool perf = false;
+    for (int i = 1; i < argc; i++) perf = perf || std::strcmp(argv[i], "-perf") == 0;
     int ndev = 0;
     if (tcsc_hip_device_count(&ndev) != TSG_OK || ndev == 0) {
         std::printf("plugin_ref_check: built and linked against the reference headers; no HIP device, not run\n");
@@ -81,6 +99,16 @@ int main(int argc, char **argv)
 
     // the lines a maintainer adds to main.cpp
     auto sf_csc = std::make_shared<TCSC>(W_raw.data(), K, N);                            // main.cpp:63
+    // "BaseTCSC" first, the speedup baseline (main.cpp:10,76-81): the oracle's
+    // restatement of comp.h:25-69 over the reference ctor's arrays
+    add_function([sf_csc](float *X, float *B, float *Y, int M, int N, int K) {
+        oracle_base_tcsc(X, sf_csc->col_start_pos.data(), sf_csc->col_start_neg.data(),
+                         sf_csc->row_index_pos.data(), sf_csc->row_index_neg.data(), B, Y, M, N, K);
+    }, "BaseTCSC");
+    add_prelu_function([sf_csc](float *X, float *B, float *alpha, float *Y, int M, int N, int K) {
+        oracle_base_tcsc_prelu(X, sf_csc->col_start_pos.data(), sf_csc->col_start_neg.data(),
+                               sf_csc->row_index_pos.data(), sf_csc->row_index_neg.data(), B, alpha, Y, M, N, K);
+    }, "BaseTCSC_PreLU");
     add_function(tsg::make_hip_comp_func(*sf_csc, K, N), "HipBaseTCSC");
     auto sf_blocked = std::make_shared<BlockedTCSC<512>>(W_raw.data(), K, N);            // main.cpp:69
     add_function(tsg::make_hip_comp_func(*sf_blocked, K, N), "HipBaseBlockedTCSC");
@@ -149,6 +177,28 @@ int main(int argc, char **argv)
             std::printf("Test case %s failed!\n", funcNames_prelu[i].c_str());
             return 1;
         }
+    }
+    if (!perf) return 0;
+    std::fflush(stdout);
+
+    // main.cpp:253-293, the reference's benchmark loop around its perf_test
+    // (perf.cpp, compiled unmodified): cycles per call, speedup vs BaseTCSC
+    const int nonZero = s;  // main.cpp passes the sparsity argument as nonZero
+    float base_cycles = 0;
+    for (size_t i = 0; i < userFuncs.size(); i++) {
+        const float perf_val = perf_test(userFuncs[i], M, K, N, nonZero);
+        std::cout << "\nRunning: " << "\x1b[31m" << funcNames[i] << "\x1b[0m" << std::endl;
+        std::cout << perf_val << " cycles" << std::endl;
+        if (funcNames[i] == "BaseTCSC") base_cycles = perf_val;
+        std::cout << "Speedup is: " << "\x1b[32m" << base_cycles / perf_val << "\x1b[0m" << std::endl;
+    }
+    float base_cycles_prelu = 0;
+    for (size_t i = 0; i < userFuncs_prelu.size(); i++) {
+        const float perf_val = perf_test_prelu(userFuncs_prelu[i], M, K, N, nonZero);
+        std::cout << "\nRunning: " << "\x1b[31m" << funcNames_prelu[i] << "\x1b[0m" << std::endl;
+        std::cout << perf_val << " cycles" << std::endl;
+        if (funcNames_prelu[i] == "BaseTCSC_PreLU") base_cycles_prelu = perf_val;
+        std::cout << "Speedup is: " << "\x1b[32m" << base_cycles_prelu / perf_val << "\x1b[0m" << std::endl;
     }
     return 0;
 }

@@ -15,7 +15,8 @@ grids of the same kernel (the host-pointer comp_func pipeline launches M
 chunks, bench.py e2e_host_pointers) under "<kernel> [grid G]", so per-launch
 figures never mix launch sizes.  The kernel-trace dispatches get the same
 split (<round>_kernel_trace_by_grid.json: count and average duration per
-grid).
+grid), with the median and, leaving out the first STEADY_SKIP launches of
+each grid (the clock ramp after idle), the steady-state average and median.
 """
 import collections
 import csv
@@ -25,6 +26,7 @@ import os
 import shutil
 import sys
 
+STEADY_SKIP = 30  # launches on the ramping clock (~25 at configs[2], profiles/r02c_clock_ramp.txt)
 src, dst = sys.argv[1], sys.argv[2]
 M, K, N, s = (int(v) for v in sys.argv[3:7])
 os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
@@ -40,12 +42,24 @@ if trace:
             w.writeheader()
             w.writerows(rows)
         by = collections.defaultdict(list)
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
         for r in rows:
             by[(r["Kernel_Name"].split("(")[0].replace("void ", "").strip(), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))].append(
                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-        json.dump({f"{k} [grid {g}]": {"dispatches": len(v), "avg_us": sum(v) / len(v) / 1e3,
-                                        "min_us": min(v) / 1e3, "max_us": max(v) / 1e3}
-                   for (k, g), v in sorted(by.items())},
+        def med(v):
+            v = sorted(v)
+            return (v[(len(v) - 1) // 2] + v[len(v) // 2]) / 2
+
+        def entry(v):
+            # launch order = trace order; the first STEADY_SKIP launches of a
+            # grid run on the ramping clock after idle (DESIGN.md 5 "Clock
+            # warm-up"): the steady-state figures leave them out
+            steady = v[STEADY_SKIP:] if len(v) > 2 * STEADY_SKIP else v
+            return {"dispatches": len(v), "avg_us": sum(v) / len(v) / 1e3, "median_us": med(v) / 1e3,
+                    "steady_dispatches": len(steady), "steady_avg_us": sum(steady) / len(steady) / 1e3,
+                    "steady_median_us": med(steady) / 1e3, "min_us": min(v) / 1e3, "max_us": max(v) / 1e3}
+
+        json.dump({f"{k} [grid {g}]": entry(v) for (k, g), v in sorted(by.items())},
                   open(dst + "_kernel_trace_by_grid.json", "w"), indent=1)
 
 # per (pass, kernel, counter): total and dispatches; a counter collected in

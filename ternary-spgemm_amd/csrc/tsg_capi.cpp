@@ -61,6 +61,9 @@ struct tsg_tcsc {
     int tile_rows = 0;                    // tcsc_hip_set_tile_rows: 0 auto, 128 or 64 (jit images)
     int jit_force = 0;                    // tcsc_hip_set_jit_width / TSG_JIT_NW: 0 = auto
     uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
+    // images that failed to load or probe at a call (bit variant_bit): calls
+    // that pick them run the 128-row 64 x 8 image loaded at registration
+    uint32_t bad_variants = 0;
     // small-M kernel (tsg_ell.hip): one sliced-ELL image per variant, built on
     // the first call (or tcsc_hip_reserve) that picks the variant
     struct EllVariant {
@@ -249,6 +252,12 @@ tsg_tcsc::JitVariant &variant_of(tsg_tcsc *h, const JitShape &sh)
 {
     if (sh.r64 && sh.half) return h->jv64h[width_index(sh.nw) - 1];
     return sh.r64 ? h->jv64[shape_index(sh.nw, sh.waves)] : h->jv[shape_index(sh)];
+}
+
+// bit of a shape in tsg_tcsc::bad_variants: 128-row 0..7, 64-row 8..15, half ring 16..18
+int variant_bit(const JitShape &sh)
+{
+    return sh.r64 && sh.half ? 16 + width_index(sh.nw) - 1 : (sh.r64 ? 8 : 0) + shape_index(sh);
 }
 
 // Shape (stream width x waves per workgroup) for a call with M rows.  Every
@@ -472,6 +481,26 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
     return sh;
 }
 
+// The image and shape a jit call with M rows runs: the automatic (or pinned)
+// pick, unless that image failed to load at an earlier call -- then the
+// 128-row 64 x 8 image loaded at registration (run_dev's fallback).
+// A call may fall back from an image that cannot be loaded to the registered
+// 128-row 64 x 8 image when nothing pinned its image or shape (a pinned
+// request fails loudly instead: TSG_ERR_HIP).
+bool may_fall_back(const tsg_tcsc *h, const JitShape &sh)
+{
+    const bool is_default = !sh.r64 && !sh.far && sh.nw == tsg::kJitNW && sh.waves == tsg::kJitWaves;
+    return !is_default && !h->tile_rows && !h->jit_force && h->far_mode != 2 && h->jv[0].mod.function &&
+           !tsg::knob_value("TSG_JIT_ROWS64_MAXM") && !tsg::knob_value("TSG_JIT_NW");
+}
+
+JitShape call_shape(const tsg_tcsc *h, int M)
+{
+    const JitShape sh = pick_jit_shape(h, M, pick_rows64(h, M));
+    if (((h->bad_variants >> variant_bit(sh)) & 1u) && may_fall_back(h, sh)) return JitShape{tsg::kJitNW, tsg::kJitWaves};
+    return sh;
+}
+
 // Tile map groups (tsg_jit_map.h) per call: gn column tiles x gm M tiles per
 // XCD group, 32 workgroups (the XCD's CUs).  Measured
 // (profiles/r03_map_density_ab.txt, r02_jit_map_bench_ab.txt):
@@ -670,8 +699,11 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     const int64_t jit_wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                             ((h->N + 8 * tsg::kJitWaves - 1) / (8 * tsg::kJitWaves));
     const bool starved = one8 && M <= kEllStarvedMaxM && jit_wgs <= kEllStarvedWgs;
-    static const char *env_max = tsg::knob_value("TSG_ELL_MAXM");  // A/B of the small-M boundary
-    const int auto_max = env_max ? atoi(env_max) : kEllAutoMaxM;
+    static const int env_max = [] {  // TSG_ELL_MAXM: A/B of the small-M boundary (not of the small-W rule)
+        const char *e = tsg::knob_value("TSG_ELL_MAXM");
+        return e ? atoi(e) : -1;
+    }();
+    const int auto_max = env_max >= 0 ? env_max : kEllAutoMaxM;
     // a small W (M x nnz <= 420 M) keeps the walk up to M = 128 while K fits
     // one chunk: the 64-row image streams its whole code image and stages X
     // (~13 us of step overhead against ~6) whatever M is, the walk's cost
@@ -680,7 +712,7 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // 41.0; (96, 4096, 16384) s = 16 61.3 vs 77.9; beyond it the image wins:
     // (128, 4096, 16384) s = 16 80.3 vs 76.1, (64, 4096, 16384) s = 8 66.2 vs
     // 63.0, s = 4 at M = 48 101 vs 71)
-    const bool small_w = !env_max && one8 && M <= kEllSmallWMaxM &&
+    const bool small_w = one8 && M <= kEllSmallWMaxM &&
                          (double)M * (double)(h->nnz_pos + h->nnz_neg) <= kEllSmallWWork;
     if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) && !starved && !small_w)
         return -1;
@@ -791,9 +823,25 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         }
         return TSG_OK;
     }
-    const bool r64 = pick_rows64(h, M);
-    const JitShape sh = h->kind == tsg_tcsc::kJit ? pick_jit_shape(h, M, r64) : JitShape{0, 0};
-    const bool half = sh.half;
+    JitShape sh = h->kind == tsg_tcsc::kJit ? call_shape(h, M) : JitShape{0, 0};
+    if (h->kind == tsg_tcsc::kJit && !variant_of(h, sh).mod.function) {
+        if (capturing)
+            return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(sh.nw) +
+                                         " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
+        rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far, sh.r64, sh.half);
+        if (rc == TSG_ERR_HIP && may_fall_back(h, sh)) {
+            // an image the loader refuses (or whose probe fails): this and later
+            // calls that pick it run the 128-row 64 x 8 image registered at
+            // tcsc_hip_create -- same result bit for bit, another speed
+            std::fprintf(stderr, "[ternary_spgemm] warning: %s; running the 128-row 64 x 8 image instead\n",
+                         g_tsg_host_err.c_str());
+            h->bad_variants |= 1u << variant_bit(sh);
+            sh = JitShape{tsg::kJitNW, tsg::kJitWaves};
+        } else if (rc) {
+            return rc;
+        }
+    }
+    const bool r64 = sh.r64, half = sh.half;
     const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM,
               chunk = r64 ? (half ? tsg::kJit64HalfChunk : tsg::kJit64Chunk) : tsg::kJitChunk;
     int Mp, Kp;
@@ -801,11 +849,6 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     tsg_tcsc::JitVariant *jv = nullptr;
     if (h->kind == tsg_tcsc::kJit) {
         jv = &variant_of(h, sh);
-        if (!jv->mod.function && capturing)
-            return fail(TSG_ERR_ARG, "M=" + std::to_string(M) + " runs the width-" + std::to_string(sh.nw) +
-                                         " image, which is not compiled yet; call tcsc_hip_reserve before capturing");
-        rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far, r64, half);
-        if (rc) return rc;
         // the stream steps through X^T chunks with a 32-bit stride, and the grid
         // (one workgroup per M tile x column tile) must stay under 2^32 threads
         const int64_t wgs = (int64_t)(Mp / tile_m) * (jv->Npad / (jv->nw * jv->waves));
@@ -1158,15 +1201,15 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
     const bool jit_fits = jit_est < 3.0 * (double)(1ull << 30);
     const std::string kname = kenv ? kenv : (jit_fits ? "jit" : "rx");
     if (kname != "jit" && kname != "rx") {
-        delete h;
+        free_handle(h);  // destroys the handle's stream too
         return fail(TSG_ERR_ARG, "TSG_KERNEL=" + kname + ": expected jit or rx");
     }
     if (B && kname != "jit") {
-        delete h;
+        free_handle(h);
         return fail(TSG_ERR_ARG, "BlockedTCSC runs on the jit kernel only (TSG_KERNEL=" + kname + ")");
     }
     if ((kname == "jit" || B) && !jit_fits) {
-        delete h;
+        free_handle(h);
         return fail(TSG_ERR_ARG, "TSG_KERNEL=jit: W has too many nonzeros for one weight-compiled image "
                                  "(> ~300M); shard columns across handles or use TSG_KERNEL=rx");
     }
@@ -1333,9 +1376,14 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
     for (int r = 1; r <= ranges; r++) {
         for (const int m : {(r - 1) * tsg::kJit64TileM + 1, std::min(std::max(max_M, 1), r * tsg::kJit64TileM)}) {
             if (pick_ell_variant(h, m) >= 0) continue;  // the small-M kernel (its images below)
-            const bool r64 = pick_rows64(h, m);
-            const JitShape sh = pick_jit_shape(h, m, r64);
-            rc = ensure_jit_variant(h, sh.nw, sh.waves, nullptr, sh.far, r64, sh.half);
+            const JitShape sh = call_shape(h, m);
+            rc = ensure_jit_variant(h, sh.nw, sh.waves, nullptr, sh.far, sh.r64, sh.half);
+            if (rc == TSG_ERR_HIP && may_fall_back(h, sh)) {  // as run_dev
+                std::fprintf(stderr, "[ternary_spgemm] warning: %s; running the 128-row 64 x 8 image instead\n",
+                             g_tsg_host_err.c_str());
+                h->bad_variants |= 1u << variant_bit(sh);
+                rc = TSG_OK;
+            }
             if (rc) return rc;
         }
     }
@@ -1368,13 +1416,13 @@ extern "C" int tcsc_hip_set_jit_width(tsg_tcsc *h, int width)
 extern "C" int tcsc_hip_jit_width(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
-    return pick_jit_shape(h, M, pick_rows64(h, M)).nw;
+    return call_shape(h, M).nw;
 }
 
 extern "C" int tcsc_hip_jit_waves(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
-    return pick_jit_shape(h, M, pick_rows64(h, M)).waves;
+    return call_shape(h, M).waves;
 }
 
 extern "C" int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows)
@@ -1391,7 +1439,7 @@ extern "C" int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows)
 extern "C" int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
-    return pick_rows64(h, M) ? tsg::kJit64TileM : tsg::kJitTileM;
+    return call_shape(h, M).r64 ? tsg::kJit64TileM : tsg::kJitTileM;
 }
 
 // Opt-in page-locking of a caller's host buffer (X or Y of repeated
@@ -1441,8 +1489,9 @@ extern "C" int tcsc_hip_set_far(tsg_tcsc *h, int mode)
 
 extern "C" int tcsc_hip_call_far(const tsg_tcsc *h, int M)
 {
-    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0 || pick_rows64(h, M)) return 0;
-    return pick_jit_shape(h, M).far ? 1 : 0;
+    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
+    const JitShape sh = call_shape(h, M);
+    return !sh.r64 && sh.far ? 1 : 0;
 }
 
 extern "C" int tcsc_hip_set_small_m(tsg_tcsc *h, int mode)
@@ -1497,7 +1546,7 @@ extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)
     if (!h) return "";
     const int ev = pick_ell_variant(h, M);
     if (ev >= 0) return use_ell_pc(h, ev) ? "tsg_tcsc_ell_pc_kernel" : "tsg_tcsc_ell_kernel";
-    if (h->kind == tsg_tcsc::kJit && pick_rows64(h, M)) return "tsg_jit64_kernel";
+    if (h->kind == tsg_tcsc::kJit && call_shape(h, M).r64) return "tsg_jit64_kernel";
     return h->kind == tsg_tcsc::kJit ? "tsg_jit_kernel" : "tsg_tcsc_rx_kernel";
 }
 
@@ -1508,8 +1557,7 @@ extern "C" int64_t tcsc_hip_call_image_bytes(tsg_tcsc *h, int M)
     const int ev = pick_ell_variant(h, M);
     if (ev >= 0) return h->ell[ev].ready ? h->ell[ev].bytes : 0;
     if (h->kind != tsg_tcsc::kJit) return (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
-    const bool r64 = pick_rows64(h, M);
-    const tsg_tcsc::JitVariant &v = variant_of(h, pick_jit_shape(h, M, r64));
+    const tsg_tcsc::JitVariant &v = variant_of(h, call_shape(h, M));
     return v.mod.function ? v.code_bytes + v.wcode_words * 4 : 0;
 }
 

@@ -627,35 +627,71 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
 // ------------------------------------------------------------ code object --
 namespace {
 
-// The dispatcher of a stream width: lib/tsg_jit.co (kJitNW columns per wave)
-// or lib/tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile);
-// 4-wave workgroups: lib/tsg_jit_w<nw>_4w.co (TSG_JIT_WAVES=4); the 64-row
-// image: lib/tsg_jit64_w<nw>[_4w].co (TSG_JIT_ROWS64=1), its half ring
-// lib/tsg_jit64h_w<nw>.co (4 waves, TSG_JIT_HALF=1).
-std::string template_path(int nw, int waves, bool r64, bool half)
+// The dispatcher of a stream width: tsg_jit.co (kJitNW columns per wave) or
+// tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile); 4-wave
+// workgroups: tsg_jit_w<nw>_4w.co (TSG_JIT_WAVES=4); the 64-row image:
+// tsg_jit64_w<nw>[_4w].co (TSG_JIT_ROWS64=1), its half ring
+// tsg_jit64h_w<nw>.co (4 waves, TSG_JIT_HALF=1).
+std::string template_name(int nw, int waves, bool r64, bool half)
 {
-    const std::string name = r64 && half ? "tsg_jit64h_w" + std::to_string(nw) + ".co"
-                             : r64 ? "tsg_jit64_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co"
-                             : nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
-                             : "tsg_jit_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co";
-    if (const char *dir = knob_value("TSG_JIT_DIR")) return std::string(dir) + "/" + name;  // tests: rx fallback
-    Dl_info info;
-    if (dladdr(reinterpret_cast<void *>(&build_jit_code), &info) && info.dli_fname) {
-        std::string p(info.dli_fname);
-        const size_t s = p.rfind('/');
-        return (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/" + name;
+    return r64 && half ? "tsg_jit64h_w" + std::to_string(nw) + ".co"
+           : r64 ? "tsg_jit64_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co"
+           : nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
+           : "tsg_jit_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co";
+}
+
+}  // namespace
+}  // namespace tsg
+
+// Every dispatcher code object, embedded in this library at build time
+// (csrc/gen_co_embed.py, Makefile): {file name, bytes, size}, null-terminated.
+struct TsgCoEntry {
+    const char *name;
+    const unsigned char *data;
+    uint64_t size;
+};
+extern "C" const TsgCoEntry tsg_co_table[];
+
+namespace tsg {
+namespace {
+
+// The template bytes: from TSG_JIT_DIR when set (tests: a directory with some
+// objects missing exercises the fallbacks), else the copy embedded in the
+// library, else the file next to the library (a build without the table
+// entry).
+std::string read_template(int nw, int waves, bool r64, bool half, std::vector<unsigned char> &img)
+{
+    const std::string name = template_name(nw, waves, r64, half);
+    std::string path;
+    if (const char *dir = knob_value("TSG_JIT_DIR")) {
+        path = std::string(dir) + "/" + name;
+    } else {
+        for (const TsgCoEntry *e = tsg_co_table; e->name; e++)
+            if (name == e->name) {
+                img.assign(e->data, e->data + e->size);
+                return "";
+            }
+        Dl_info info;
+        path = name;
+        if (dladdr(reinterpret_cast<void *>(&build_jit_code), &info) && info.dli_fname) {
+            const std::string p(info.dli_fname);
+            const size_t s = p.rfind('/');
+            path = (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/" + name;
+        }
     }
-    return name;
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return "cannot open jit template " + path;
+    img.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return "";
 }
 
 }  // namespace
 
 std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves, bool r64, bool half)
 {
-    const std::string path = template_path(nw, waves, r64, half);
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return "cannot open jit template " + path;
-    std::vector<unsigned char> img((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    std::vector<unsigned char> img;
+    const std::string rerr = read_template(nw, waves, r64, half, img);
+    if (!rerr.empty()) return rerr;
     if (img.size() < sizeof(Elf64_Ehdr)) return "jit template too small";
     Elf64_Ehdr eh;
     std::memcpy(&eh, img.data(), sizeof eh);

@@ -81,3 +81,41 @@ def test_configs4_shards_on_one_gpu(tsg):
     torch.cuda.synchronize()
     for r in range(P):
         assert torch.equal(Yfull[:, r * w:(r + 1) * w].view(torch.int32), G[r].view(torch.int32)), f"block {r}"
+
+
+def _oracle_threads():
+    import os
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(16, n or len(os.sched_getaffinity(0))))
+
+
+@pytest.mark.timeout(900)
+def test_configs4_shards_fractional_x(tsg, oracle_mod):
+    """The eight configs[4] rank workloads with ORDER-SENSITIVE X (24-bit
+    mantissas over a 2^-23..2^0 exponent spread: every partial sum rounds),
+    EVERY element of every shard compared bitwise with the BaseTCSC
+    restatement (oracle/tcsc_oracle.c, comp.h:37-63) run over all 4096 rows
+    with OpenMP: the shards are other W matrices than configs[2]'s, so their
+    accumulation order is pinned here, not only by the integer-X test above
+    (where any order gives the same bits)."""
+    import torch
+    import tsg_dist as D
+    O = oracle_mod
+    w = NTOT // P
+    X = O.init_x_frac(M, K, 77)
+    Xd = torch.from_numpy(X).cuda()
+    b_full = ((np.arange(NTOT, dtype=np.float32) % 13) - 6) * np.float32(0.37)
+    th = _oracle_threads()
+    for r in range(P):
+        csp, csn, rip, rin = D.ShardedTCSC.draw(K, NTOT, S, SEED, r, P, "weak")
+        sh = D.ShardedTCSC((csp, csn, rip, rin), K, NTOT, r, P, device=0, already_sliced=True)
+        b = np.ascontiguousarray(b_full[sh.n0:sh.n1])
+        Yr = sh.forward(Xd, torch.from_numpy(b_full).cuda()).cpu().numpy()
+        kernel = sh.local.call_kernel(M)
+        sh.local.close()
+        ref = O.base_tcsc(X, O.TCSC(csp, csn, rip, rin, K, w), b, threads=th)
+        diff = Yr.view(np.uint32) != ref.view(np.uint32)
+        assert not diff.any(), f"rank {r}: {int(diff.sum())} of {M * w} elements differ ({kernel})"

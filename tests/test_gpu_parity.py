@@ -352,6 +352,40 @@ def test_failed_image_load_falls_back_to_rx(tsg, oracle_mod, monkeypatch, capfd)
         tsg.TCSCDevice(*t.arrays, K, N)
 
 
+def test_missing_64row_dispatcher_falls_back_to_128row(tsg, oracle_mod, monkeypatch, capfd, tmp_path):
+    """VERDICT r04 "next" 5 / ADVICE r04: with a dispatcher directory that
+    holds only the 128-row template (an older install), a configs[2]-shaped
+    call -- the 64-row 128 x 8 image by default -- runs the 128-row image
+    registered at tcsc_hip_create, with a warning on stderr, and is still
+    bit-exact; later calls and the plan queries report the image that runs.
+    A pinned 64-row image fails loudly instead."""
+    import shutil
+    import torch
+    O = oracle_mod
+    libdir = os.path.join(os.path.dirname(tsg.LIB_PATH))
+    shutil.copy(os.path.join(libdir, "tsg_jit.co"), tmp_path / "tsg_jit.co")
+    monkeypatch.setenv("TSG_JIT_DIR", str(tmp_path))
+    M, K, N, s = 4096, 4096, 2048, 4
+    csp, csn, rip, rin = tsg.gen_tcsc(K, N, s, 42)
+    t = O.TCSC(csp, csn, rip, rin, K, N)
+    h = tsg.TCSCDevice(csp, csn, rip, rin, K, N)
+    assert h.kernel_name() == "tsg_jit_kernel"          # registration: the 128-row image loaded
+    assert h.call_kernel(M) == "tsg_jit64_kernel"       # the automatic plan picks the 64-row image
+    X = O.init_x_frac(M, K, 31)
+    b = (np.arange(N, dtype=np.float32) % 13 - 6) * np.float32(0.37)
+    Y = h.gemm_torch(torch.from_numpy(X).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+    assert "running the 128-row 64 x 8 image instead" in capfd.readouterr().err
+    assert h.call_kernel(M) == "tsg_jit_kernel" and h.call_tile_rows(M) == 128
+    ref = O.base_tcsc(X, t, b, threads=16)
+    assert _bits_eq(Y, ref)
+    Y2 = h.gemm_torch(torch.from_numpy(X).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+    assert _bits_eq(Y2, ref) and "warning" not in capfd.readouterr().err  # no retry per call
+    h.set_tile_rows(64)  # pinned: no fallback
+    with pytest.raises(tsg.TSGError, match="cannot open jit template"):
+        h.gemm_torch(torch.from_numpy(X).cuda(), torch.from_numpy(b).cuda())
+    h.close()
+
+
 def test_gpu_encoder_matches_host_ctor(tsg, oracle_mod):
     """GPU-side TCSC encoder == the TCSC ctor (TCSC.h:13-41)
     array for array, incl. the 4x4 KAT, values other than +-1 (zeros there),
@@ -441,11 +475,31 @@ def test_plugin_against_reference_headers():
     # N=4096 s=4, "./sparseGEMM.out -correctness") and configs[1] (M=512
     # K=4096 N=4096 s=4): the reference's own generator, ctors, serial dense
     # GEMM and compare_results (main.cpp:192-247) around the HIP comp_funcs
+    # "-perf" (configs[0] and configs[1]) then runs the reference's own
+    # benchmark loop (main.cpp:253-293) with its perf_test (perf.cpp compiled
+    # unmodified, -DCALIBRATE rdtsc path): "Running: / cycles / Speedup is:"
+    # per comp_func, the speedup relative to "BaseTCSC" (main.cpp:10)
+    import re
     for argv in ([], ["-M", "130", "-K", "1100", "-N", "300", "-s", "2"],
-                 ["-M", "32", "-K", "1024", "-N", "4096", "-s", "4"],
-                 ["-M", "512", "-K", "4096", "-N", "4096", "-s", "4"]):
+                 ["-M", "32", "-K", "1024", "-N", "4096", "-s", "4", "-perf"],
+                 ["-M", "512", "-K", "4096", "-N", "4096", "-s", "4", "-perf"]):
         r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=400)
         assert r.returncode == 0, r.stdout + r.stderr
-        for name in ("HipBaseTCSC", "HipBaseBlockedTCSC", "HipBaseTCSC_PreLU"):
+        for name in ("BaseTCSC", "HipBaseTCSC", "HipBaseBlockedTCSC", "BaseTCSC_PreLU", "HipBaseTCSC_PreLU"):
             assert f"Test case {name} passed!" in r.stdout, r.stdout
         assert "DataStructureInterface round trip passed!" in r.stdout
+        if "-perf" not in argv:
+            continue
+        # main.cpp:257-263's three lines per function, as run_benchmark.py:63-67 scrapes them
+        runs = re.findall(r"Running: \x1b\[31m(\w+)\x1b\[0m\n([0-9.e+]+) cycles\nSpeedup is: \x1b\[32m([0-9.e+]+)\x1b\[0m",
+                          r.stdout)
+        got = {name: (float(cyc), float(sp)) for name, cyc, sp in runs}
+        assert sorted(got) == sorted(["BaseTCSC", "HipBaseTCSC", "HipBaseBlockedTCSC", "BaseTCSC_PreLU",
+                                      "HipBaseTCSC_PreLU"]), r.stdout
+        assert got["BaseTCSC"][1] == 1.0 and got["BaseTCSC_PreLU"][1] == 1.0
+        for name in ("HipBaseTCSC", "HipBaseBlockedTCSC", "HipBaseTCSC_PreLU"):
+            assert got[name][0] > 0 and got[name][1] > 1.0, (name, got[name])  # the GPU beats one CPU core
+        out = os.environ.get("TSG_REF_PERF_OUT")  # keep the report (profiles/r05_ref_perf_test.txt)
+        if out:
+            with open(out, "a") as f:
+                f.write(f"$ oracle/_ref/plugin_ref_check {' '.join(argv)}\n{r.stdout}\n")
