@@ -1,9 +1,10 @@
 #!/bin/bash
-# GPU box, round 5: the tests this round touched (image fallback, the
-# reference's perf_test loop around the HIP comp_funcs, configs[4] shards with
-# fractional X, RCCL pipeline), smoke(), the default bench line and the
-# 8-rank gloo rehearsal of the world > 1 line (compute + all-gather).
-# Usage: scripts/r05_check.sh <tag>
+# GPU box: a batch of GPU tests (TESTS="..." pytest arguments; default: the
+# files round 5 touched -- the image fallback, the reference's perf_test loop
+# around the HIP comp_funcs, configs[4] shards with fractional X, the RCCL
+# pipeline), smoke(), the default bench line and the 8-rank gloo rehearsal of
+# the world > 1 line (compute + all-gather).
+#   [TESTS="tests/x.py -k y"] bash scripts/check.sh <tag>
 set -o pipefail
 TAG=${1:-r05a}
 export TMPDIR=/tmp

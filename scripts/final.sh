@@ -1,15 +1,15 @@
 #!/bin/bash
-# GPU box, round-3 final evidence: the whole GPU suite, the default bench line,
-# rocprofv3 --kernel-trace --stats of the exact default bench command plus PMC
-# passes of it (scripts/profile_gpu.sh), and PMC passes of configs[1]
-# (HBM bytes per launch).  Summaries under gpurun_out/summary_<tag>*.
-# Usage: scripts/r03_final.sh <tag> [skip-suite]
+# GPU box, a round's final evidence: the whole GPU suite, the default bench
+# line, rocprofv3 --kernel-trace --stats of the exact default bench command
+# plus PMC passes of it (scripts/profile_gpu.sh), and PMC passes of
+# configs[1] (HBM bytes per launch).  Summaries under gpurun_out/summary_<tag>*.
+#   bash scripts/final.sh <tag> [skip-suite]
 set -o pipefail
-TAG=${1:-r03final}
+TAG=${1:?tag}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ "$2" != skip-suite ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 170 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
   rc=$?; echo "gpu suite rc=$rc: $(tail -1 gpurun_out/pytest_$TAG.log)"; [ $rc -eq 0 ] || { tail -30 gpurun_out/pytest_$TAG.log; exit $rc; }
 fi
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.jsonl 2> gpurun_out/bench_$TAG.err

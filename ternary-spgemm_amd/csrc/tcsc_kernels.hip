@@ -162,6 +162,46 @@ __global__ __launch_bounds__(256) void tsg_transpose_quads_kernel(const float *_
     *reinterpret_cast<float4 *>(XQ + ((size_t)ct * units + pr) * 256 + (size_t)j * 4) = v;
 }
 
+// X [M][K] -> the staged copy of the 64-row image's ROW layout
+// (tsg_internal.h kJit64RowFlag): (chunk c, M tile t) is 47 KiB at (c * Mt +
+// t) * 47 KiB, rows of 47 quads (752 B) -- row r holds X[64 t + r][kb .. kb +
+// 187], kb = c * 188 (the last chunk: K - 188 when K >= 188 and K % 4 == 0,
+// jit64_row_kbase), zero past M and K.  Each 16-B slot is 16 contiguous bytes
+// of a row of X, so this is a gather-copy of row runs (no transpose): reads
+// and writes both run along rows.  Four workgroups per (chunk, M tile), 752
+// slots each.  HBM-bound: 2 * 4 * Mp * Kp bytes.
+template <bool VEC>
+__global__ __launch_bounds__(256) void tsg_transpose_rows_kernel(const float *__restrict__ X,
+                                                                 float *__restrict__ XR, int M, int K, int Mp,
+                                                                 int nch)
+{
+    constexpr int kQ = 47, kSlots = 64 * kQ, kPer = kSlots / 4;  // 752 slots per workgroup
+    const int Mt = Mp >> 6;
+    const int blk = blockIdx.x, part = blk & 3, tc = blk >> 2;
+    // workgroup order (M tile * nch + chunk) * 4 + part: the workgroups in
+    // flight read a few M tiles' rows end to end
+    const int t = tc / nch, c = tc % nch;
+    const int kb = (c == nch - 1 && K >= 4 * kQ && (K & 3) == 0) ? K - 4 * kQ : c * 4 * kQ;
+    float *dst = XR + ((size_t)c * Mt + t) * (kSlots * 4);
+    for (int i = threadIdx.x; i < kPer; i += 256) {
+        const int slot = part * kPer + i, r = slot / kQ, q = slot % kQ;
+        const int m = 64 * t + r, k = kb + 4 * q;
+        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (m < M) {
+            const float *row = X + (size_t)m * K;
+            if (VEC) {
+                if (k < K) v = *reinterpret_cast<const float4 *>(row + k);  // K % 4 == 0: whole quad inside
+            } else {
+                if (k < K) v.x = row[k];
+                if (k + 1 < K) v.y = row[k + 1];
+                if (k + 2 < K) v.z = row[k + 2];
+                if (k + 3 < K) v.w = row[k + 3];
+            }
+        }
+        *reinterpret_cast<float4 *>(dst + (size_t)slot * 4) = v;
+    }
+}
+
 // One LDS-DMA piece: 64 lanes x 16 B from per-lane global addresses to LDS
 // [lds_dst, lds_dst + 1 KiB).  Inline asm on purpose: hipcc cannot prove that
 // later ds_reads do not alias an in-flight LDS-DMA and would put
@@ -333,6 +373,17 @@ int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int 
 int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream,
                            int chunk)
 {
+    hipStream_t s = (hipStream_t)stream;
+    const bool vec = K % 4 == 0 && ((uintptr_t)X & 15) == 0;
+    if (piece_rows == 0) {  // the row layout: 188-row chunks, 47 KiB per (chunk, M tile)
+        if (chunk != 188 || Mp % 64 || Kp % 188) return -1;
+        const int nch = Kp / 188;
+        const int64_t blocks = (int64_t)nch * (Mp / 64) * 4;
+        if (blocks >= ((int64_t)1 << 31)) return -1;
+        if (vec) hipLaunchKernelGGL(tsg_transpose_rows_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, X, XQ, M, K, Mp, nch);
+        else hipLaunchKernelGGL(tsg_transpose_rows_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, X, XQ, M, K, Mp, nch);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     // Mp is a multiple of 64 (the 64-row image's M tile) and Kp of 192 (its
     // chunk): the pieces cover [0, Kp) x [0, Mp) exactly
     if ((chunk != 192 && chunk != 96) || Mp % 64 || Kp % chunk) return -1;
@@ -341,8 +392,6 @@ int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int 
     const int64_t blocks = (int64_t)(Kp / chunk) * (Mp / 64) * (units / 4);
     if (blocks >= ((int64_t)1 << 31)) return -1;
     dim3 grid((unsigned)blocks);
-    const bool vec = K % 4 == 0 && ((uintptr_t)X & 15) == 0;
-    hipStream_t s = (hipStream_t)stream;
     if (piece_rows == 16) {
         if (vec) hipLaunchKernelGGL((tsg_transpose_quads_kernel<true, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp, units);
         else hipLaunchKernelGGL((tsg_transpose_quads_kernel<false, 16>), grid, dim3(256), 0, s, X, XQ, M, K, Mp, Kp, units);

@@ -47,7 +47,7 @@ struct tsg_tcsc {
     // call with an M that picks them (or tcsc_hip_reserve)
     struct JitVariant {
         int nw = 0, waves = 0, Npad = 0;
-        int piece_rows = 0;               // 64-row image: rows per DMA piece (its X^T layout)
+        int piece_rows = 0;               // 64-row image: rows per DMA piece (its X^T layout; 0 = row layout)
         int nch = 0, chunk = 0;           // X^T chunks of the image and K rows per chunk
         tsg::JitModule mod;               // dispatcher + generated code, loaded
         uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
@@ -164,7 +164,7 @@ int dims_for(const tsg_tcsc *h, int M, int &Mp, int &Kp, bool r64 = false, bool 
     const bool jit = h->kind == tsg_tcsc::kJit;
     const int tm = !jit ? tsg::kRxTileM : r64 ? tsg::kJit64TileM : tsg::kJitTileM;
     Mp = ((std::max(M, 1) + tm - 1) / tm) * tm;
-    const int c64 = half ? tsg::kJit64HalfChunk : tsg::kJit64Chunk;
+    const int c64 = tsg::jit64_chunk(half);
     const int nch64 = std::max(1, (h->K + c64 - 1) / c64);
     Kp = !jit ? h->rimg.nch * tsg::kRxChunk : r64 ? nch64 * c64 : h->jit_nch * tsg::kJitChunk;
     return TSG_OK;
@@ -314,18 +314,29 @@ bool far_xt(const tsg_tcsc *h, int M)
 // 78.9-79.5, M = 512 (64 x 8, s = 4) 208-209 / 215 vs 202-205 / 217-220
 // (r04f_shape_ab.jsonl, r04g_bound_ab.jsonl).  TSG_JIT_XDIRECT=1 / 0 forces it
 // on (where possible) / off, read per call (A/B).
-bool x_direct_auto(const tsg_tcsc *h, int nw)
+// Row layout (round 5, tsg_internal.h kJit64RowFlag): its pieces read runs of
+// contiguous row bytes, as fast from X as from the staged copy
+// (profiles/r05_dma_stride_micro.txt), so every call that can reads X
+// directly (K >= 188, K % 4 == 0, X 16-B aligned): no X^T pass, no work
+// buffer.  The blocked layout keeps the round-4 rule above.
+bool x_direct_auto(const tsg_tcsc *h, int nw, int piece_rows)
 {
+    if (piece_rows == 0) return true;
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
     return (double)nw * density >= kXDirectMinAddsPerRow;
+}
+
+// K (and X) allow direct X for a 64-row image with this piece shape
+bool x_direct_shape_ok(int K, int piece_rows)
+{
+    return piece_rows == 0 ? K >= tsg::kJit64RowChunk && K % 4 == 0 : K > 0 && K % (256 / piece_rows) == 0;
 }
 
 bool x_direct(const tsg_tcsc *h, const float *dX, int M, int K, const tsg_tcsc::JitVariant &jv)
 {
     const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
-    const bool on = e ? e[0] == '1' : x_direct_auto(h, jv.nw);
-    const int pr = jv.piece_rows;
-    return on && K > 0 && pr > 0 && K % (256 / pr) == 0 && ((uintptr_t)dX & 15) == 0 &&
+    const bool on = e ? e[0] == '1' : x_direct_auto(h, jv.nw, jv.piece_rows);
+    return on && x_direct_shape_ok(K, jv.piece_rows) && ((uintptr_t)dX & 15) == 0 &&
            (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
 }
 
@@ -388,7 +399,8 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     // configs[2] 1239.4 vs 1248.8 us per step with integer X
     // (r04z_direct_big_ab.jsonl); the sparse end is the 64-row image's either
     // way (s = 16: 468 vs 569 int, 496 vs 600 frac).
-    const bool direct_capable = h->K % (256 / tsg::jit64_piece_rows()) == 0 && x_direct_auto(h, tsg::kJit64WideNW);
+    const bool direct_capable = x_direct_shape_ok(h->K, tsg::jit64_piece_rows()) &&
+                                x_direct_auto(h, tsg::kJit64WideNW, tsg::jit64_piece_rows());
     if ((density <= 0.1875 || h->K >= 8192 || direct_capable) && pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW)
         return true;
     if (s.nw != tsg::kJitNW || s.waves != tsg::kJitWaves) return true;
@@ -843,7 +855,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     }
     const bool r64 = sh.r64, half = sh.half;
     const int tile_m = r64 ? tsg::kJit64TileM : tsg::kJitTileM,
-              chunk = r64 ? (half ? tsg::kJit64HalfChunk : tsg::kJit64Chunk) : tsg::kJitChunk;
+              chunk = r64 ? tsg::jit64_chunk(half) : tsg::kJitChunk;
     int Mp, Kp;
     dims_for(h, M, Mp, Kp, r64, half);
     tsg_tcsc::JitVariant *jv = nullptr;
@@ -858,6 +870,14 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     // the 64-row image stages straight from row-major X (no X^T pass, no work
     // buffer) when every row starts 16-B aligned and the offsets fit 32 bits
     const bool direct = r64 && x_direct(h, dX, M, K, *jv);
+    if (r64 && jv->chunk != chunk)  // the image and this call's X^T dims must agree (TSG_JIT_QBLOCK read at both)
+        return fail(TSG_ERR_ARG, "64-row image built for " + std::to_string(jv->chunk) + "-row chunks, call expects " +
+                                     std::to_string(chunk) + " (TSG_JIT_QBLOCK changed after the image was built)");
+    // row layout, direct X: the last chunk starts at K - 188, lastadj bytes
+    // below its slot (tsg_internal.h jit64_row_kbase)
+    const int lastadj = direct && jv->piece_rows == 0
+                            ? 4 * ((jv->nch - 1) * tsg::kJit64RowChunk - tsg::jit64_row_kbase(K, jv->nch, jv->nch - 1))
+                            : 0;
     if (!direct) {
         rc = ensure_work(h, M, capturing, r64, half);
         if (rc) return rc;
@@ -889,7 +909,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                jv->nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
-                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0)
+                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0, lastadj)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)

@@ -131,7 +131,37 @@ constexpr uint32_t kJit64Format = 3;                    // region header word 7 
 // row) instead of 8 rows x 8 quads (whole 128-B lines per row; 2-way bank
 // conflicts on ds_read_b128).  TSG_JIT_QBLOCK=16|8 picks (A/B).
 constexpr uint32_t kJit64R16Flag = 1u << 18;
-int jit64_piece_rows();  // 16 (default) or 8 (TSG_JIT_QBLOCK=8); tsg_jit.cpp
+// Row layout (round 5, the default; region header word 7 bit 20): the LDS
+// buffer holds the tile's 64 rows row-major, 47 quads (188 K rows, 752 B) per
+// row -- quad q of row r at r * 752 + q * 16.  752 / 4 = 188 = -4 (mod 64), so
+// the 16 lanes of every ds_read_b128 lane group (rows r, distinct r mod 16)
+// read 16 distinct 16-B bank slots: conflict-free (ds_read_b64 / b32 as the
+// blocked layout).  A lane's base is r * 752 plus one uniform offset q * 16
+// per quad.  The chunk is 47 KiB = pieces 0 .. 46 of the 48-KiB ring buffer;
+// DMA lane j of piece pr carries slot 64 pr + j = (row, quad) = divmod(., 47),
+// so a piece reads one to three runs of contiguous row bytes: straight from
+// row-major X ("direct X") as fast as from a staged copy
+// (profiles/r05_dma_stride_micro.txt: 0.81 vs 0.85 us per 48-KiB step, against
+// 1.55 for the blocked layout's 16-row x 64-B pieces).  The last chunk starts
+// at K - 188 (when K >= 188 and K % 4 == 0; jit64_row_kbase), so direct X
+// never reads past a row's end; the staged copy (tsg_transpose_rows_kernel)
+// holds the same bytes.
+constexpr uint32_t kJit64RowFlag = 1u << 20;
+constexpr int kJit64RowQuads = 47;
+constexpr int kJit64RowChunk = 4 * kJit64RowQuads;           // 188 K rows
+constexpr int kJit64RowPitch = 16 * kJit64RowQuads;          // 752 B per M row in LDS
+// first K row of chunk c of nch (row layout): c * 188, the last chunk K - 188
+inline int jit64_row_kbase(int K, int nch, int c)
+{
+    const bool shift = c == nch - 1 && K >= kJit64RowChunk && K % 4 == 0;
+    return shift ? K - kJit64RowChunk : c * kJit64RowChunk;
+}
+// rows per DMA piece of the blocked layout (16, 8: TSG_JIT_QBLOCK), or 0: the
+// row layout (default); tsg_jit.cpp
+int jit64_piece_rows();
+// K rows per chunk of the 64-row image: the row layout 188, the blocked
+// layout 192, the half ring 96
+inline int jit64_chunk(bool half) { return half ? 96 : jit64_piece_rows() ? 192 : kJit64RowChunk; }
 // Half ring (64-row image, 4-wave workgroups only; region header word 7 bit
 // 19): 96-row chunks of 24 pieces (24 KiB), a 72-KiB ring, so two workgroups
 // share a CU and each SIMD runs two waves (a lone wave issues its VOP2 adds
@@ -164,7 +194,7 @@ constexpr int kJitTailPadWords = 32768 + 1024;
 struct JitImage {
     int K = 0, N = 0, Npad = 0, nch = 0, B = 0, nw = 0, waves = kJitWaves;
     int tile_m = kJitTileM, chunk = kJitChunk;  // 64 / kJit64Chunk for the 64-row image
-    int piece_rows = 0;                          // 64-row image: rows per DMA piece (16 or 8)
+    int piece_rows = 0;                          // 64-row image: rows per DMA piece (16 or 8; 0 = row layout)
     bool half = false;                           // 64-row image: the half ring (kJit64HalfChunk)
     std::vector<uint32_t> code;    // region: [magic x2][0][0] then one stream per (tile, wave)
     std::vector<uint32_t> wcode;   // per (column tile, stream): byte offset of the stream
@@ -184,10 +214,12 @@ struct JitModule {
                      bool rows64 = false, bool half = false);  // "" on success
     void unload();
 };
+// xrow > 0: the 64-row image stages straight from X (xrow floats per row);
+// lastadj: bytes the row layout's last chunk starts below its slot (direct X)
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                     int prelu, uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask,
-                    void *stream, int tile_m = kJitTileM, int xrow = 0);  // xrow > 0: 64-row image staging straight from X
+                    void *stream, int tile_m = kJitTileM, int xrow = 0, int lastadj = 0);
 int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream);
 
 // ---------------------------------------------------------------------------
@@ -247,7 +279,8 @@ int launch_transpose(const float *X, float *XT, int M, int K, int Mp, int Kp, vo
 // X [M][K] -> X^T in the k-pair layout of the jit kernel (Kp even, Mp even)
 int launch_transpose_pairs(const float *X, float *XP, int M, int K, int Mp, int Kp, void *stream);
 // X [M][K] -> the blocked k-quad layout of the 64-row image (Mp % 64 == 0, Kp % 192 == 0;
-// piece_rows 16 or 8, kJit64R16Flag)
+// piece_rows 16 or 8, kJit64R16Flag), or with piece_rows 0 its row layout's
+// staged copy (kJit64RowFlag; Kp % 188 == 0)
 int launch_transpose_quads(const float *X, float *XQ, int M, int K, int Mp, int Kp, int piece_rows, void *stream,
                            int chunk = kJit64Chunk);
 int launch_tcsc_rx(const float *XT, int Mp, const uint32_t *wstart, const uint32_t *ent,

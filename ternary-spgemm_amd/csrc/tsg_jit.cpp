@@ -117,6 +117,11 @@ struct Emit {
         c.push_back(0x80545254u);
         c.push_back(0x82558055u);
     }
+    void base_last_adj()                              // s[84:85] -= s87 (row layout: the last chunk starts at K - 188)
+    {
+        c.push_back(0x80d45754u);
+        c.push_back(0x82d58055u);
+    }
     void touch_addr(uint32_t region_off)              // s[88:89] = s[92:93] + off
     {
         align8();
@@ -239,7 +244,7 @@ std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw, int C = k
 int jit64_piece_rows()
 {
     const char *v = knob_value("TSG_JIT_QBLOCK");
-    return v && v[0] == '8' ? 8 : 16;
+    return !v ? 0 : v[0] == '8' ? 8 : 16;
 }
 
 void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
@@ -253,12 +258,17 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     if (r64) far = false;
     // K rows per chunk and per LDS unit (a pair, or a quad in the 64-row image):
     // 48 units of 1 KiB per chunk either way
-    const int CH = r64 ? (half ? kJit64HalfChunk : kJit64Chunk) : kJitChunk, U = r64 ? 4 : 2;
-    const uint32_t kBuf = (uint32_t)(CH / U) * kPairBytes;  // one LDS ring buffer (48 KiB; half ring 24)
-    // 64-row image: rows per DMA piece PR (16 or 8) and quads per piece 64 / PR
-    // (tsg_internal.h, kJit64R16Flag)
-    const int PR = r64 ? jit64_piece_rows() : 0, PQ = r64 ? 64 / PR : 0;
-    const JitRegs R(waves, CH / U);
+    // the 64-row image's row layout (default; tsg_internal.h kJit64RowFlag) or
+    // its blocked layout (TSG_JIT_QBLOCK; the half ring always)
+    const bool rowlay = r64 && !half && jit64_piece_rows() == 0;
+    const int CH = r64 ? (half ? kJit64HalfChunk : rowlay ? kJit64RowChunk : kJit64Chunk) : kJitChunk,
+              U = r64 ? 4 : 2;
+    // one LDS ring buffer: 48 KiB (row layout: 47 KiB used), half ring 24
+    const uint32_t kBuf = rowlay ? 48u * 1024u : (uint32_t)(CH / U) * kPairBytes;
+    // 64-row image, blocked layout: rows per DMA piece PR (16 or 8) and quads
+    // per piece 64 / PR (tsg_internal.h, kJit64R16Flag); 0 = the row layout
+    const int PR = r64 && !rowlay ? (jit64_piece_rows() ? jit64_piece_rows() : 16) : 0, PQ = PR ? 64 / PR : 0;
+    const JitRegs R(waves, rowlay ? 48 : CH / U);  // (row layout: 47 pieces, the register contract of 48)
     const int streams = waves;  // one stream per wave (no M split)
     const int kPieces = R.pieces;
     const uint32_t kLane128V = R.lane128, kAcc0 = R.acc0;
@@ -328,7 +338,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                              (uint32_t)streams | (uint32_t)kJitMSplit << 8, (uint32_t)B, (uint32_t)S,
                              (uint32_t)kJitRing | (r64 ? kJit64Format : kJitFormat) << 8 |
                                  (uint32_t)(m0k ? kJitM0kFlag : 0u) | (far ? kJitFarFlag : 0u) |
-                                 (PR == 16 ? kJit64R16Flag : 0u) | (half ? kJit64HalfFlag : 0u)});
+                                 (PR == 16 ? kJit64R16Flag : 0u) | (half ? kJit64HalfFlag : 0u) |
+                                 (rowlay ? kJit64RowFlag : 0u)});
     const char *na = knob_value("TSG_JIT_NOALIGN");
     Emit E{code, !(na && na[0] == '1')};
     // TSG_JIT_CP="dma,touch": cache-policy bits of the LDS-DMA pieces and the
@@ -373,7 +384,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // per row the columns with an entry there
     auto build_section = [&](int q, Section &sec) {
         const StepSpec &sp = plan[(size_t)q];
-        const int p = sp.pass, kc = sp.chunk * CH;
+        // first K row of the chunk in LDS (row layout: the last chunk starts at K - 188)
+        const int p = sp.pass, kc = rowlay ? jit64_row_kbase(K, nch, sp.chunk) : sp.chunk * CH;
         const int32_t *cs = p ? csn : csp, *ri = p ? rin : rip;
         if (sp.reset)
             for (int col = sp.c0; col < sp.c1; col++) {
@@ -413,6 +425,12 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             for (int i = base_chunk; i < j; i++) E.base_next();
         }
         base_chunk = j;
+        if (rowlay && j == nch - 1 && jit64_row_kbase(K, nch, j) != j * CH) {
+            // direct X: the last chunk starts s87 = 4 (188 nch - K) bytes below its
+            // slot (the staged copy holds it in its slot: s87 = 0); a later
+            // chunk never follows it without a base reset
+            E.base_last_adj();
+        }
         E.nop(4);  // SALU-written SGPR base -> VMEM
     };
     int vm_step = 0;  // VMEM operations (DMA pieces, code touches) issued in the current step
@@ -424,8 +442,9 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         // the dispatcher may then stage straight from row-major X, whose rows
         // end at K (tsg_jit_kernel.hip "direct X", K % (4 PQ) == 0).  They are
         // a suffix of the wave's pieces, so no M0 group loses its first piece.
-        if (r64 && (int64_t)plan[(size_t)q].chunk * CH + 4 * PQ * (((int64_t)cur_wave * kPieces + i) / (64 / PR)) >= K)
-            return;
+        if (rowlay ? cur_wave * kPieces + i >= kJit64RowQuads
+                   : r64 && (int64_t)plan[(size_t)q].chunk * CH + 4 * PQ * (((int64_t)cur_wave * kPieces + i) / (64 / PR)) >= K)
+            return;  // (row layout: the chunk's 47 pieces; piece 47 of the register contract is never staged)
         const uint32_t sub = m0k ? (uint32_t)(i & 3) : 0u;
         if (sub == 0) {
             E.m0_wave((uint32_t)(q % kJitRing) * kBuf + (uint32_t)i * kPairBytes);
@@ -503,9 +522,11 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     const uint32_t lb = kLdsBaseV + (uint32_t)(rq % kJitRing);
                     // 64-row image, blocked k-quad layout: quad q of the chunk at
                     // (q / PQ) * 64 KiB / PR + (q % PQ) * 16 PR B from the lane's base
-                    const uint32_t off = r64 ? (uint32_t)(rd.pair / PQ) * (65536u / (uint32_t)PR) +
-                                                   (uint32_t)(rd.pair % PQ) * 16u * (uint32_t)PR
-                                             : (uint32_t)rd.pair * kPairBytes;
+                    // row layout: quad q at the lane's row base + 16 q
+                    const uint32_t off = rowlay ? (uint32_t)rd.pair * 16u
+                                         : r64 ? (uint32_t)(rd.pair / PQ) * (65536u / (uint32_t)PR) +
+                                                     (uint32_t)(rd.pair % PQ) * 16u * (uint32_t)PR
+                                               : (uint32_t)rd.pair * kPairBytes;
                     if (r64) {
                         const QuadRead qr = quad_read(rd.mask);
                         if (qr.nreg == 4) E.ds_read_b128(dst, lb, off);
@@ -779,12 +800,12 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream)
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
                     uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask, void *stream,
-                    int tile_m, int xrow)
+                    int tile_m, int xrow, int lastadj)
 {
     int mtiles = Mp / tile_m, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
-                      (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask, (void *)&xrow};
+                      (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask, (void *)&xrow, (void *)&lastadj};
     hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.function, (unsigned)(mtiles * ntiles), 1, 1,
                                          (unsigned)waves * 64u, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;

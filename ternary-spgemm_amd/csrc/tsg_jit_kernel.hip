@@ -36,8 +36,9 @@
 //   v[116:244) accumulators, column c at v116 + 2c (rows 2l, 2l+1 of the lane)
 //   s[80:81] X^T base, s82 chunk stride in bytes, s83 LDS byte offset of this
 //   wave's first DMA piece, s[84:85] chunk base (stream),
-//   s86 saved M0, s[88:89] prefetch address (stream), s[92:93] region base,
-//   s[94:95] return address.
+//   s86 saved M0, s87 bytes the 64-row row layout's last chunk starts below
+//   its slot (direct X; else 0), s[88:89] prefetch address (stream),
+//   s[92:93] region base, s[94:95] return address.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -92,6 +93,7 @@ constexpr uint32_t kJM0kFlag = 1u << 16;  // header word 7: piece offsets in the
 constexpr uint32_t kJFormat = kJRows64 ? 3u : 2u;  // header word 7 bits 8-15: the X^T layout the code expects
 constexpr uint32_t kJR16Flag = 1u << 18;            // header word 7: 64-row image pieces of 16 rows x 4 quads
 constexpr uint32_t kJHalfFlag = 1u << 19;           // header word 7: the half ring
+constexpr uint32_t kJRowFlag = 1u << 20;            // header word 7: the 64-row image's row layout (188-row chunks)
 #if TSG_JIT_ROWS64
 #define TSG_JIT_KERNEL_NAME tsg_jit64_kernel
 #else
@@ -157,7 +159,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
-    int tmask, int xrow)
+    int tmask, int xrow, int lastadj)
 {
     __shared__ __attribute__((aligned(16))) char lds[kJRing * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -195,8 +197,12 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     // layout, PR rows per piece: row r at (r / PR) KiB + (r % PR) * 16;
     // tsg_internal.h)
     const uint32_t pr_rows = (hdr[7] & kJR16Flag) ? 16u : 8u;
-    const uint32_t lb0 = kJRows64 ? ((uint32_t)lane / pr_rows) * 1024u + ((uint32_t)lane % pr_rows) * 16u
-                                  : (uint32_t)lane * 16u;
+    // row layout (tsg_internal.h kJit64RowFlag): row r at r * 752 B
+    // (uniform: the SGPR stride and chunk adjustment below depend on it)
+    const bool rowlay = kJRows64 && !kJHalf && (__builtin_amdgcn_readfirstlane(hdr[7]) & kJRowFlag) != 0;
+    const uint32_t lb0 = rowlay   ? (uint32_t)lane * 752u
+                         : kJRows64 ? ((uint32_t)lane / pr_rows) * 1024u + ((uint32_t)lane % pr_rows) * 16u
+                                    : (uint32_t)lane * 16u;
     const uint32_t lb1 = lb0 + kJBufBytes, lb2 = lb0 + 2 * kJBufBytes;
     // LDS-DMA piece i of this wave = pair row pr = wave * P + i of the chunk: the
     // lane's 16 B at ((pr * Mp/2) + m0/2 + lane) * 16 from the chunk base (64-row
@@ -224,6 +230,13 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
         uint32_t o;
         if (!kJRows64) {
             o = (pr * ((uint32_t)Mp / 2u) + (uint32_t)m0 / 2u + (uint32_t)lane) * 16u;
+        } else if (rowlay) {
+            // slot 64 pr + lane = (row, quad) of the 64 x 47-quad chunk; pieces
+            // pr >= 47 are never staged (their offset only has to be valid)
+            const uint32_t slot = min(pr * 64u + (uint32_t)lane, 64u * 47u - 1u);
+            const uint32_t row = slot / 47u, quad = slot % 47u;
+            o = direct ? (uint32_t)min(m0 + (int)row, M - 1) * xrow_b + quad * 16u + 3072u
+                       : ((uint32_t)mt * 47u + pr) * 1024u + (uint32_t)lane * 16u;
         } else if (direct) {
             const uint32_t rgs = 64u / pr_rows;  // row groups per tile = quads per piece
             const uint32_t row = (uint32_t)min(m0 + (int)((pr % rgs) * pr_rows + (uint32_t)lane % pr_rows), M - 1);
@@ -242,7 +255,11 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     const uint32_t l128 = (mt & tmask) == 0 ? (uint32_t)lane * 128u : 0u;
     // chunk stride: kJChunk K rows of X^T (both staged layouts: Mp * chunk * 4
     // bytes), or of one row-major X row (direct)
-    const uint32_t stride = direct ? (uint32_t)kJChunk * 4u : (uint32_t)kJChunk * (uint32_t)Mp * 4u;
+    // (row layout: 188-row chunks; the staged copy holds 47 KiB per (chunk, M tile))
+    const uint32_t chunk_rows = rowlay ? 188u : (uint32_t)kJChunk;
+    const uint32_t stride = direct ? chunk_rows * 4u : chunk_rows * (uint32_t)Mp * 4u;
+    // row layout, direct X: the last chunk starts lastadj bytes below its slot (K - 188)
+    const uint32_t adj = direct ? (uint32_t)lastadj : 0u;
 
 #define TSG_JIT_CALL(...)                                                                           \
     asm volatile("s_getpc_b64 s[94:95]\n"                                                           \
@@ -252,7 +269,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
                  "s_setpc_b64 %[cp]\n"                                                              \
                  ".Ljb%=:"                                                                          \
                  : __VA_ARGS__                                                                      \
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(xbase), "{s82}"(stride), "{s83}"(wb), \
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(xbase), "{s82}"(stride), "{s83}"(wb), "{s87}"(adj), \
                    TSG_JIT_IN                                                                       \
                  : TSG_JIT_CLOBBERS)
 #if TSG_JIT_ROWS64  // one accumulator VGPR per column (acc0 = v116; 4 waves: v122, half ring v116)

@@ -66,7 +66,8 @@ def test_plan_matches_measured_winners(tsg, shape, plan):
     (512, 4096, 16384, "tsg_jit64_kernel"),
     (1536, 4096, 16384, "tsg_jit64_kernel"),      # 128-row 64 x 8 in 1.5 rounds (547 vs 617 us, r04h)
     (2048, 4096, 16384, "tsg_jit64_kernel"),      # dense, short K: 128 x 8, direct X (kernels 615 vs 617 us int, r04o)
-    (4096, 4100, 16384, "tsg_jit_kernel"),        # ... K % 16 != 0: no direct X, the 128-row image
+    (4096, 4100, 16384, "tsg_jit64_kernel"),      # ... the row layout reads X directly for K % 4 == 0 (round 5)
+    (4096, 4098, 16384, "tsg_jit_kernel"),        # ... K % 4 != 0: no direct X, the 128-row image
     (32, 1024, 4096, "tsg_tcsc_ell_kernel"),      # configs[0]
     (16, 16384, 16384, "tsg_tcsc_ell_kernel"),    # K in several chunks: up to 16 (184 vs 247 us, r04g)
     (17, 16384, 16384, "tsg_jit64_kernel"),       # (M = 32: 310 vs 248 us)

@@ -128,20 +128,24 @@ def test_rows64_full_y_configs2_kn(tsg, oracle_mod, M):
     h.close()
 
 
-@pytest.mark.parametrize("qblock", ["16", "8"])
-@pytest.mark.parametrize("M,K", [(1, 1024), (64, 4096), (130, 1000), (37, 192 * 3), (70, 208), (70, 196)])
+@pytest.mark.parametrize("qblock", ["rows", "16", "8"])
+@pytest.mark.parametrize("M,K", [(1, 1024), (64, 4096), (130, 1000), (37, 192 * 3), (70, 208), (70, 196),
+                                 (70, 188), (70, 376), (64, 189), (5, 190), (130, 4100)])
 def test_rows64_direct_x_and_staged(tsg, oracle_mod, monkeypatch, M, K, qblock):
-    """The 64-row image stages its DMA pieces straight from row-major X when
-    asked to (TSG_JIT_XDIRECT=1; automatic above one 64-row tile), the rows
-    are 16-B aligned and no piece straddles K (tsg_jit_kernel.hip "direct X":
-    no X^T pass), and through the blocked staged copy otherwise: X at a
-    4-byte offset takes the staged path.  Both piece shapes of the
-    blocked layout (TSG_JIT_QBLOCK: 16 rows x 4 quads, 8 x 8).  Bit-exact
-    against the oracle (rows past M read row M-1 and are dropped; pieces past
-    K are never staged)."""
+    """The 64-row image stages its DMA pieces straight from row-major X
+    (TSG_JIT_XDIRECT=1; automatic for the row layout, tsg_internal.h
+    kJit64RowFlag) when the rows are 16-B aligned and K allows it (row layout:
+    K >= 188 and K % 4 == 0, the last chunk starting at K - 188; blocked
+    layout: no piece straddles K), and through the staged copy otherwise
+    (TSG_JIT_XDIRECT=0, or X at a 4-byte offset).  The row layout and both
+    piece shapes of the blocked layout (TSG_JIT_QBLOCK: 16 rows x 4 quads, 8 x
+    8).  Bit-exact against the oracle (rows past M read row M-1 and are
+    dropped; blocked pieces past K are never staged)."""
     import torch
-    monkeypatch.setenv("TSG_JIT_QBLOCK", qblock)
-    monkeypatch.setenv("TSG_JIT_XDIRECT", "1")
+    if qblock == "rows":
+        monkeypatch.delenv("TSG_JIT_QBLOCK", raising=False)
+    else:
+        monkeypatch.setenv("TSG_JIT_QBLOCK", qblock)
     O = oracle_mod
     N = 333
     t = O.tcsc_encode(O.gen_ternary(K, N, 4, M + K))
@@ -150,12 +154,14 @@ def test_rows64_direct_x_and_staged(tsg, oracle_mod, monkeypatch, M, K, qblock):
     b = torch.linspace(-2, 2, N).cuda()
     ref = O.base_tcsc(Xh, t, b.cpu().numpy())
     buf = torch.empty(M * K + 4, device="cuda")
-    for shift in (0, 1):  # 0: 16-B aligned (direct when K % 4 == 0); 1: 4-byte offset (staged)
-        X = buf[shift:shift + M * K].view(M, K)
-        X.copy_(torch.from_numpy(Xh))
-        Y = h.gemm_torch(X, b)
-        torch.cuda.synchronize()
-        assert _bits_eq(Y.cpu().numpy(), ref), (M, K, shift)
+    for direct in ("1", "0"):
+        monkeypatch.setenv("TSG_JIT_XDIRECT", direct)
+        for shift in (0, 1):  # 0: 16-B aligned (direct when K allows); 1: 4-byte offset (staged)
+            X = buf[shift:shift + M * K].view(M, K)
+            X.copy_(torch.from_numpy(Xh))
+            Y = h.gemm_torch(X, b)
+            torch.cuda.synchronize()
+            assert _bits_eq(Y.cpu().numpy(), ref), (M, K, shift, direct, qblock)
     h.close()
 
 

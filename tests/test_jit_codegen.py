@@ -44,16 +44,20 @@ class Geom:
         # DMA pieces take their in-group offset from the instruction offset (one
         # M0 per 4 pieces; the dispatcher subtracts it from the global offsets)
         self.m0k = (int(code[7]) >> 16) & 1
-        # 16 m0k, 17 far, 18 R16, 19 the half ring (64-row image, 4 waves, 96-row chunks)
-        assert int(code[7]) >> 20 == 0 and (self.r64 or (int(code[7]) >> 18) & 3 == 0)
+        # 16 m0k, 17 far, 18 R16, 19 the half ring (64-row image, 4 waves, 96-row chunks),
+        # 20 the row layout (64-row image: rows of 47 quads, 188-row chunks)
+        assert int(code[7]) >> 21 == 0 and (self.r64 or (int(code[7]) >> 18) & 7 == 0)
         self.half = (int(code[7]) >> 19) & 1
+        self.rowlay = (int(code[7]) >> 20) & 1
         assert not self.half or (self.waves == 4 and self.chunk == 96)
+        assert not self.rowlay or (self.chunk == 188 and not self.half and not (int(code[7]) >> 18) & 1)
         self.unit = 4 if self.r64 else 2              # k rows per LDS unit (quad / pair)
-        self.pairs = self.chunk // self.unit          # units per chunk
+        self.pairs = self.chunk // self.unit          # units per chunk (row layout: 47 quads per row)
         self.pair_bytes = self.tile_m * 4 * self.unit  # one unit row of the tile in LDS: 1 KiB
         assert self.pair_bytes == 1024
-        self.buf_bytes = self.pairs * self.pair_bytes
-        self.pieces = self.pairs // self.waves        # DMA pieces (pair rows) per wave
+        # ring buffer: 48 KiB (row layout: 47 pieces used of the 48 the register contract has)
+        self.buf_bytes = 48 * 1024 if self.rowlay else self.pairs * self.pair_bytes
+        self.pieces = self.buf_bytes // 1024 // self.waves  # DMA pieces (pair rows) per wave
         self.lds_v = 8 + 4 * self.slots               # X slots: 4 VGPRs each
         self.sink_v = self.lds_v + self.ring
         self.dma_v = self.sink_v + 1
@@ -123,7 +127,7 @@ def _decode(code, pc, G):
         return "wait_lgkm", ((w0 >> 8) & 0xF,), 1
     if (w0 & 0xFFFFFFF0) == 0xBF8C0F70:  # s_waitcnt vmcnt(n), n <= 15
         return "wait_vm", (w0 & 0xF,), 1
-    simple = {0xBF8A0000: "barrier", 0xBED6007C: "save_m0",
+    simple = {0xBF8A0000: "barrier", 0xBED6007C: "save_m0", 0x80D45754: "last_adj", 0x82D58055: "last_adjc",
               0xBEFC0056: "restore_m0", 0xBED40150: "base_reset", 0xBE801D5E: "ret", 0x82558055: "base_addc",
               0x8259805D: "touch_addc", 0x80545254: "base_add"}
     if w0 in simple:
@@ -160,7 +164,9 @@ def _overlaps(reads, r0, n):
 
 def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
     """One workgroup (column tile t, M tile at m0) over the k-pair X^T XP
-    [pairs][Mp/2][4]: returns acc[tile rows, tile cols]."""
+    [pairs][Mp/2][4] (64-row image: quads [Kp/4][Mp][4]; row layout: per chunk
+    [Mp][47][4], XP[j] = the quads from the chunk's first K row,
+    jit64_row_kbase): returns acc[tile rows, tile cols]."""
     G = Geom(code)
     WAVES, NW, PAIRS, PAIR_BYTES, BUF_BYTES, PIECES = (G.waves, G.nw, G.pairs, G.pair_bytes, G.buf_bytes,
                                                        G.pieces)
@@ -168,8 +174,8 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
     stride = G.chunk * Mp * 4
     NBUF = G.ring
     lds = np.zeros(NBUF * BUF_BYTES // 4, np.float32)
-    landed = np.full(NBUF * PAIRS, -1)   # phase a pair row's data landed
-    last_read = np.full(NBUF * PAIRS, -1)
+    landed = np.full(NBUF * BUF_BYTES // PAIR_BYTES, -1)   # phase a 1-KiB piece's data landed
+    last_read = np.full(NBUF * BUF_BYTES // PAIR_BYTES, -1)
     S = G.streams
     waves = [Wave(w, int(wcode[t * S + w]) // 4) for w in range(WAVES)]
     RPL = 1 if G.r64 else 2  # M rows per lane
@@ -202,6 +208,10 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     wv.base = XT_BASE
                 elif kind == "base_add":
                     wv.base += stride
+                elif kind == "last_adj":  # s87: 0 for a staged copy (the one emulated here)
+                    assert G.rowlay
+                elif kind == "last_adjc":
+                    assert G.rowlay
                 elif kind == "touch_addr":
                     wv.touch = f[0]
                 elif kind == "touch":
@@ -218,7 +228,11 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     assert rem == 0 and 0 <= j < nch
                     dst = wv.m0 + off  # the offset applies to the LDS address too
                     assert dst % BUF_BYTES == pr * PAIR_BYTES, "DMA lands on the wrong pair row"
-                    if G.r64:  # blocked k-quad piece pr = Q qg + rg: lane slot l = row R rg + l % R, quad Q qg + l / R
+                    if G.rowlay:  # lane slot 64 pr + l = (row, quad) of the 64 x 47-quad chunk
+                        assert pr < PAIRS, "row layout: piece past the chunk's 47"
+                        slots = pr * 64 + np.arange(64)
+                        data = XP[j][m0 + slots // PAIRS, slots % PAIRS].reshape(-1).copy()
+                    elif G.r64:  # blocked k-quad piece pr = Q qg + rg: lane slot l = row R rg + l % R, quad Q qg + l / R
                         R = G.pr_rows
                         Q = 64 // R
                         qg, rg = divmod(pr, Q)
@@ -248,7 +262,18 @@ def emulate_tile(code, wcode, t, XP, m0, Mp, nch):
                     assert 8 <= vd and vd + nreg <= 8 + 4 * G.xslots and (vd - 8) % 4 == 0
                     allowed = {4: (0,), 2: (0, 8), 1: (0, 4, 8, 12)}[nreg]
                     buf = a - G.lds_v
-                    if G.r64:
+                    if G.rowlay:
+                        # row layout: lane l's base (dispatcher) = buffer + l * 752; quad q at + 16 q
+                        sub = off % 16
+                        assert sub in allowed and off // 16 < PAIRS
+                        lanes = np.arange(64)
+                        addr = buf * BUF_BYTES + lanes * 16 * PAIRS + off
+                        pieces = np.unique(addr // PAIR_BYTES)
+                        assert all(0 <= landed[p] < phase for p in pieces), "LDS read of data not yet landed before a barrier"
+                        for p in pieces:
+                            last_read[p] = max(last_read[p], phase)
+                        wv.v[vd:vd + nreg] = np.stack([lds[addr // 4 + t] for t in range(nreg)])
+                    elif G.r64:
                         # blocked k-quad layout: lane l's base (dispatcher) = buffer +
                         # (l / R) KiB + (l % R) * 16; quad q at (q / Q) * 64 KiB / R + (q % Q) * 16 R
                         R = G.pr_rows
@@ -323,7 +348,15 @@ def emulate(code, wcode, X, K, N):
     Mp = -(-max(M, 1) // TM) * TM
     XT = np.zeros((nch * CHUNK, Mp), np.float32)
     XT[:K, :M] = X.T
-    XP = to_quads(XT) if G.r64 else to_pairs(XT)
+    if G.rowlay:  # per chunk: the quads from its first K row (the last chunk: K - 188 when K >= 188, K % 4 == 0)
+        XT0 = np.zeros((nch * CHUNK + CHUNK, Mp), np.float32)
+        XT0[:K, :M] = X.T
+        XP = []
+        for j in range(nch):
+            kb = K - CHUNK if (j == nch - 1 and K >= CHUNK and K % 4 == 0) else j * CHUNK
+            XP.append(to_quads(XT0[kb:kb + CHUNK]).transpose(1, 0, 2).copy())  # [Mp][47][4]
+    else:
+        XP = to_quads(XT) if G.r64 else to_pairs(XT)
     ntiles = len(wcode) // G.streams
     Y = np.zeros((Mp, ntiles * TILE_COLS), np.float32)
     for t in range(ntiles):
@@ -423,6 +456,30 @@ def test_jit_code_64row_image(tsg, oracle_mod, M, K, N, s, width, waves):
     integer and order-sensitive X, one add per nonzero."""
     for frac in (False, True):
         _check(tsg, oracle_mod, M, K, N, s, 5 + K + N + width, frac, width=width, waves=waves, rows64=True)
+
+
+@pytest.mark.parametrize("layout", ["rows", "16", "8"])
+@pytest.mark.parametrize("M,K,N,s", [(64, 188, 70, 4), (70, 376, 40, 2), (5, 189, 30, 4), (33, 1000, 24, 8),
+                                     (64, 192, 64, 4), (9, 4096, 16, 8)])
+def test_jit_code_64row_layouts(tsg, oracle_mod, monkeypatch, layout, M, K, N, s):
+    """The 64-row image's LDS layouts: the row layout (default, round 5: rows
+    of 47 quads, 188-row chunks, the last chunk starting at K - 188 when K >=
+    188 and K % 4 == 0) and the blocked layouts (TSG_JIT_QBLOCK=16 / 8, 192-row
+    chunks) -- K on and around the chunk boundaries, every element bit-exact."""
+    if layout != "rows":
+        monkeypatch.setenv("TSG_JIT_QBLOCK", layout)
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(K, N, s, K + N))
+    code, _ = tsg.jit_codegen64(*t.arrays, K, N, width=16, waves=4)
+    G = Geom(code)
+    assert G.rowlay == (layout == "rows") and G.chunk == (188 if layout == "rows" else 192)
+    assert G.pr_rows == (0 if layout == "rows" else 16 if layout == "16" else 8) or layout == "rows"
+    # the last-chunk adjustment (s87) is emitted exactly when the last chunk starts at K - 188
+    nch = -(-K // G.chunk)
+    shifted = layout == "rows" and K >= 188 and K % 4 == 0 and K % 188 != 0
+    assert (any(int(w) == 0x80D45754 for w in code)) == shifted
+    for frac in (False, True):
+        _check(tsg, O, M, K, N, s, 3 + K, frac, width=16, waves=4, rows64=True)
 
 
 @pytest.mark.parametrize("width,waves", [(32, 4), (16, 8), (8, 4)])
