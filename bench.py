@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--s", type=int, default=4)
     ap.add_argument("--strong", action="store_true", help="N fixed in total, split over the GPUs")
     ap.add_argument("--chunks", type=int, default=4, help="M chunks of the compute/all-gather pipeline")
-    ap.add_argument("--clock-warmup", type=float, default=0.3,
+    ap.add_argument("--clock-warmup", type=float, default=1.0,
                     help="seconds of untimed steps before the warmup steps (GPU clock ramp; 0 = none)")
     ap.add_argument("--seed-w", type=int, default=42)
     ap.add_argument("--seed-x", type=int, default=12345)
@@ -270,7 +270,7 @@ def headline(world: int, steps: int, flops_all: int, compute_elapsed_max: float,
 
 def build_line(a, *, world, mode, backend, M, K, Nr, Ntot, s, nnz, nnz_all, kname, compute_elapsed_max,
                kern_ms_max, gather=None, traffic=None, cpu=None, e2e=None, stream_ms=None, setup_s=0.0,
-               clock_warmup=(0.0, 0)) -> dict:
+               clock_warmup=(0.0, 0), kernel_timing=None) -> dict:
     """The JSON line rank 0 prints (bench.py contract), from the measured
     quantities (max over ranks).  Pure: tests/test_bench_launch.py checks it
     without a GPU."""
@@ -321,7 +321,7 @@ def build_line(a, *, world, mode, backend, M, K, Nr, Ntot, s, nnz, nnz_all, knam
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                      "traffic": traffic,
-                     "kernel": kname, "kernel_ms": round(kern_ms_max, 4),
+                     "kernel": kname, "kernel_ms": round(kern_ms_max, 4), "kernel_timing": kernel_timing,
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "kernel_gflops": round(adds / (kern_ms_max * 1e-3) / 1e9, 2),
                      "traffic_source": (os.path.relpath(PROFILE_PMC, REPO) if traffic is not None else None),
@@ -433,10 +433,16 @@ def main():
     for _ in range(a.warmup):
         h.gemm_torch(X, b, Y)
     torch.cuda.synchronize()
-    h.set_timing(True)
-    h.kernel_time(reset=True)
     barrier()
     torch.cuda.synchronize()
+    # The timed steps run WITHOUT per-launch timing events: an event pair
+    # around every launch leaves the GPU idle ~10 us per launch
+    # (profiles/r05h_step_overhead.jsonl, rocprofv3 trace: 59.2-59.7 us kernels
+    # back to back without, 58.6 us + 10.1 us gaps with, at configs[1]).  HIP
+    # events on the kernel's stream (torch's current stream: gemm_torch
+    # launches there) bracket the K steps; a step that is one launch (the
+    # kernel reads X itself: tcsc_hip_call_launches) runs its kernels back to
+    # back, so that stream time / K is the kernel's average launch duration.
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t_start = time.perf_counter()
     ev0.record(stream)
@@ -447,9 +453,21 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    kern_ms_total, launches = h.kernel_time(reset=True)
-    h.set_timing(False)
     stream_ms = ev0.elapsed_time(ev1)
+    step_launches = h.call_launches(X, M)
+    # a second pass of K steps with an event pair around every launch of the
+    # main kernel (tcsc_hip_set_timing): the kernel alone when the step also
+    # stages X^T; reported beside (it includes ~3-5 us of the events' own gap)
+    h.set_timing(True)
+    h.kernel_time(reset=True)
+    for _ in range(a.steps):
+        h.gemm_torch(X, b, Y)
+    torch.cuda.synchronize()
+    pair_ms_total, launches = h.kernel_time(reset=True)
+    h.set_timing(False)
+    pair_ms = pair_ms_total / max(launches, 1)
+    kern_ms_total = stream_ms if step_launches == 1 else pair_ms_total
+    launches = a.steps if step_launches == 1 else launches
 
     # --- world > 1: configs[4]'s whole step = the compute of this rank's
     # column block AND the RCCL all-gather of every rank's block into the
@@ -509,10 +527,10 @@ def main():
                   "bytes_received_per_gpu": 4 * M * (Ntot - Nr), "chunks": len(pipe.ranges)}
         del pipe, Yfull
 
-    tt = torch.tensor([elapsed, kern_ms_total / max(launches, 1)], device=dev, dtype=torch.float64)
+    tt = torch.tensor([elapsed, kern_ms_total / max(launches, 1), pair_ms], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    elapsed_max, kern_ms_max = float(tt[0]), float(tt[1])
+    elapsed_max, kern_ms_max, pair_ms_max = float(tt[0]), float(tt[1]), float(tt[2])
     nnz_t = torch.tensor([nnz], device=dev, dtype=torch.int64)
     if world > 1:
         dist.all_reduce(nnz_t)
@@ -571,7 +589,13 @@ def main():
         out = build_line(a, world=world, mode=mode, backend=backend, M=M, K=K, Nr=Nr, Ntot=Ntot, s=s, nnz=nnz,
                          nnz_all=nnz_all, kname=kname, compute_elapsed_max=elapsed_max, kern_ms_max=kern_ms_max,
                          gather=gather, traffic=traffic, cpu=cpu, e2e=e2e, stream_ms=stream_ms,
-                         setup_s=setup_s, clock_warmup=(clock_warmup_s, n_clock))
+                         setup_s=setup_s, clock_warmup=(clock_warmup_s, n_clock),
+                         kernel_timing={"launches_per_step": step_launches,
+                                        "kernel_ms_source": ("HIP events on the kernel's stream over the timed "
+                                                             "region / K (one launch per step, back to back)"
+                                                             if step_launches == 1 else
+                                                             "HIP event pair around every launch, second pass"),
+                                        "event_pair_kernel_ms": round(pair_ms_max, 4)})
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -139,6 +139,12 @@ int tsg_ell_build(const int32_t *col_start_pos, const int32_t *col_start_neg, co
 int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows);
 int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M);
 
+/* Device kernels a device-pointer call with M rows and this X launches: 1
+ * when the kernel reads X itself (the small-M walks; the 64-row image's
+ * direct X), 2 when an X^T staging kernel runs first.  bench.py
+ * times such a one-launch step's stream as the kernel's duration. */
+int tcsc_hip_call_launches(const tsg_tcsc *h, const float *dX, int M);
+
 /* The 64-row image's machine code (layout as tsg_jit_codegen; region header
  * word 7 format 3, the k-quad layout): width 128 / 64 / 32 / 16 / 8, waves 8
  * (or 4 for widths 32, 16, 8). */

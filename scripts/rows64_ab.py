@@ -30,6 +30,8 @@ ap.add_argument("--xint", action="store_true", help="X integer U[-512, 512] (ben
 a = ap.parse_args()
 import torch  # noqa: E402
 
+step_timed = None
+
 arrs = T.gen_tcsc(a.K, a.N, a.s, 42)
 nnz = len(arrs[2]) + len(arrs[3])
 h = T.TCSCDevice(*arrs, a.K, a.N, device=0)
@@ -38,16 +40,25 @@ VALU = 128 * 256 * 2.4e9 / 1e12  # T adds/s, v_pk_add_f32 (the VOP2 add issues a
 
 
 def timed(M, X, Y):
+    """kernel ms (HIP events around every launch) and step ms (back-to-back
+    calls with the per-kernel events OFF: the events themselves add ~8-10 us
+    between launches, profiles/r05g_event_overhead.jsonl)"""
     for _ in range(20):  # clock warm-up + warmup
         h.gemm_torch(X, b, Y)
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        h.gemm_torch(X, b, Y)
+    torch.cuda.synchronize()
+    step = (time.perf_counter() - t0) / a.reps * 1e3
     h.set_timing(True)
     h.kernel_time(reset=True)
     t0 = time.perf_counter()
     for _ in range(a.reps):
         h.gemm_torch(X, b, Y)
     torch.cuda.synchronize()
-    step = (time.perf_counter() - t0) / a.reps * 1e3
+    global step_timed
+    step_timed = (time.perf_counter() - t0) / a.reps * 1e3
     ms, n = h.kernel_time(reset=True)
     h.set_timing(False)
     return ms / max(n, 1), step
@@ -75,6 +86,7 @@ for M in (int(v) for v in a.M.split(",")):
             adds = M * (nnz + a.N)
             key = mode + ("" if not w else f"_w{w}")
             out[key] = {"kernel": h.call_kernel(M), "kernel_ms": round(ms, 5), "step_ms": round(step, 5),
+                        "step_with_events_ms": round(step_timed, 5),
                         "width": h.jit_width(M), "waves": h.jit_waves(M), "image_bytes": h.call_image_bytes(M),
                         "valu_frac_pk": round(adds / ms / 1e9 / VALU, 4)}
             if ref is None:

@@ -22,11 +22,13 @@ ap.add_argument("--N", type=int, default=16384)
 ap.add_argument("--s", type=int, default=4)
 ap.add_argument("--tile-rows", type=int, default=0)
 ap.add_argument("--reps", type=int, default=50)
+ap.add_argument("--small-m", type=int, default=0)
 a = ap.parse_args()
 import torch  # noqa: E402
 
 h = T.TCSCDevice(*T.gen_tcsc(a.K, a.N, a.s, 42), a.K, a.N, device=0)
 h.set_tile_rows(a.tile_rows)
+h.set_small_m(a.small_m)
 g = torch.Generator(device="cuda")
 g.manual_seed(12345)
 X = torch.randint(-512, 513, (a.M, a.K), generator=g, device="cuda", dtype=torch.int32).float()
@@ -41,11 +43,16 @@ for timing in (False, True, False, True):
     h.set_timing(timing)
     h.kernel_time(reset=True)
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record()
     for _ in range(a.reps):
         h.gemm_torch(X, b, Y)
+    e1.record()
     torch.cuda.synchronize()
     step = (time.perf_counter() - t0) / a.reps * 1e3
+    out.setdefault("stream_ms_timing_on" if timing else "stream_ms_timing_off", []).append(
+        round(e0.elapsed_time(e1) / a.reps, 5))
     ms, n = h.kernel_time(reset=True)
     out.setdefault("step_ms_timing_on" if timing else "step_ms_timing_off", []).append(round(step, 5))
     if timing:

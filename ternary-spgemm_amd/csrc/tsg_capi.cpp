@@ -1456,6 +1456,21 @@ extern "C" int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows)
     return TSG_OK;
 }
 
+extern "C" int tcsc_hip_call_launches(const tsg_tcsc *h, const float *dX, int M)
+{
+    if (!h || M <= 0) return 0;
+    if (pick_ell_variant(h, M) >= 0) return 1;
+    if (h->kind != tsg_tcsc::kJit) return 2;
+    const JitShape sh = call_shape(h, M);
+    if (!sh.r64) return 2;
+    // the variant's width and layout as run_dev sees them (built or not yet)
+    tsg_tcsc::JitVariant v = variant_of(const_cast<tsg_tcsc *>(h), sh);
+    v.nw = sh.nw;
+    if (!v.mod.function) v.piece_rows = sh.half ? (tsg::jit64_piece_rows() ? tsg::jit64_piece_rows() : 16)
+                                                : tsg::jit64_piece_rows();
+    return x_direct(h, dX, M, h->K, v) ? 1 : 2;
+}
+
 extern "C" int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;

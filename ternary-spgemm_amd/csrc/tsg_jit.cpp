@@ -134,6 +134,7 @@ struct Emit {
     void wait_vm0() { c.push_back(0xbf8c0f70u); }
     void wait_vm(uint32_t n) { c.push_back(0xbf8c0f70u | n); }            // s_waitcnt vmcnt(n), n <= 15
     void barrier() { c.push_back(0xbf8a0000u); }
+    void setprio(uint32_t p) { c.push_back(0xbf8f0000u | p); }  // s_setprio p (issue arbitration between waves)
     void ret() { c.push_back(0xbe801d5eu); }         // s_setpc_b64 s[94:95]
     uint32_t pos_bytes() const { return (uint32_t)(c.size() * 4); }
 };
@@ -319,6 +320,22 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     int m0k = 1, lag = 1;
     if (const char *dv = knob_value("TSG_JIT_DMA")) std::sscanf(dv, "%lf,%d,%d", &dma_spread, &m0k, &lag);
     if (lag != 2) lag = 1;
+    // Stagger (TSG_JIT_STAGGER=1, 8-wave workgroups; MI355X_MICROARCH.md "Two
+    // waves per SIMD" item 9): waves w and w + 4 share a SIMD and run the same
+    // step structure in lockstep -- their DMA issue, LDS reads and adds
+    // collide.  The first half of the waves then runs half a step AHEAD: its
+    // barrier sits in the middle of a step (after half its read groups), the
+    // DMA pieces it issues go out after that barrier and are waited for before
+    // its next one, and before it a wave reads only its current step's chunk.
+    // Barrier k then orders the early waves' mid-step k+1 with the late
+    // waves' end of step k: every ring buffer is still written only after all
+    // waves finished reading it and read only after all its pieces landed
+    // (checked by the CPU emulation, tests/test_jit_codegen.py).
+    // TSG_JIT_PRIO=1: s_setprio 1 for the waves of the second half (item 4).
+    const char *sv = knob_value("TSG_JIT_STAGGER");
+    const bool stagger = sv && sv[0] == '1' && waves == 8 && !B && lag == 1;
+    const char *pv = knob_value("TSG_JIT_PRIO");
+    const bool prio = pv && pv[0] == '1' && waves == 8;
     // X slots: all of v[8 : 104) for BaseTCSC; BlockedTCSC keeps y of half the
     // columns (nw registers) at the top of that range
     const int S = B ? (kJitXRegs - nw) / kJitSlotRegs : kJitSlots;
@@ -491,6 +508,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             n0 = t * tile_cols + w * nw;
             std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
+            const bool early = stagger && w < waves / 2;  // runs half a step ahead of waves w + 4
+            if (prio && w >= waves / 2) E.setprio(1);
             E.save_m0();
             // prologue: the first kJitRing - 1 steps staged, landed, visible
             if (steps > 0) {
@@ -586,27 +605,45 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 const int ngroups = (nrd + G - 1) / G;
                 const int qd = q + kJitRing - 1;  // the step whose chunk this step stages
                 const bool dma = qd < steps && !d_nodma;
-                // pieces go out before read groups 0 .. span-1 (span 0: all at the step start)
-                const int span = dma ? std::min(ngroups, (int)std::ceil(dma_spread * ngroups)) : 0;
+                // the stagger's early waves: the step's barrier (barrier q - 1)
+                // before read group `mid`; the DMA pieces after it
+                const int mid = early ? ngroups / 2 : 0;
+                const int ngd = ngroups - mid;  // the groups the pieces spread over
+                // pieces go out before read groups mid .. mid+span-1 (span 0: all at once)
+                const int span = dma ? std::min(ngd, (int)std::ceil(dma_spread * ngd)) : 0;
                 int pieces_out = 0;
                 auto pieces_upto = [&](int upto) {
                     for (; pieces_out < upto; pieces_out++) dma_piece(qd, pieces_out);
                     if (pieces_out == kPieces && upto == kPieces) touches();
                 };
-                if (dma) {
-                    dma_begin(qd);
-                    if (span == 0) pieces_upto(kPieces);
-                } else {
-                    touches();
-                }
+                bool released = !early;  // past this step's barrier (early waves) / after the last one
+                auto dma_start = [&] {
+                    if (early && q >= 1) {
+                        // barrier q - 1: the pieces issued in the previous step
+                        // (for step q + 1) landed first; then all waves have
+                        // finished step q - 1, whose buffer this step's DMA overwrites
+                        if (!d_novm) E.wait_vm(ntouch);
+                        if (!d_nobar) E.barrier();
+                    }
+                    released = true;
+                    if (dma) {
+                        dma_begin(qd);
+                        if (span == 0) pieces_upto(kPieces);
+                    } else {
+                        touches();
+                    }
+                };
+                if (!early) dma_start();
                 for (int i0 = 0, grp = 0; i0 < nrd; i0 += G, grp++) {
+                    if (early && grp == mid) dma_start();
                     const int i1 = std::min(nrd, i0 + G);
                     const int64_t g1 = first[q] + i1;
                     issue_reads(g1, q);  // (only if the schedule left the group unread)
                     wait_reads(g1);
-                    issue_reads(g1 + RA, lag == 2 ? q : q + 1);
-                    if (dma && grp < span && pieces_out < kPieces)  // this group's share of the pieces
-                        pieces_upto(std::min(kPieces, ((grp + 1) * kPieces + span - 1) / span));
+                    // (early waves before their barrier: this step's chunk only)
+                    issue_reads(g1 + RA, lag == 2 || !released ? q : q + 1);
+                    if (dma && grp >= mid && grp - mid < span && pieces_out < kPieces)  // this group's share
+                        pieces_upto(std::min(kPieces, ((grp - mid + 1) * kPieces + span - 1) / span));
                     // per column its entries of the group (ascending k); columns in pairs, interleaved
                     std::vector<std::vector<uint32_t>> xs(nw);
                     for (int i = i0; i < i1; i++) {
@@ -626,7 +663,14 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                             E.pk_acc(kAcc0 + 2u * (uint32_t)col, kTmp0 + 2u * (uint32_t)(col - sp.c0));
                             live[col] = 0;
                         }
+                if (!released) dma_start();  // (an early wave's step with fewer than mid + 1 read groups)
                 if (dma && pieces_out < kPieces) pieces_upto(kPieces);
+                if (early) {
+                    // no barrier at the step's end: its pieces are waited for
+                    // before the next step's mid barrier
+                    issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
+                    continue;
+                }
                 if (lag == 1) {
                     issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
                     if (!d_novm) E.wait_vm(ntouch);  // this step's pieces (the touches may run on)
@@ -637,6 +681,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 }
                 if (!d_nobar) E.barrier();
             }
+            if (early && steps > 0 && !d_nobar) E.barrier();  // barrier steps - 1 (the late waves' last)
+            if (prio && w >= waves / 2) E.setprio(0);
             E.wait_vm0();  // no load outstanding past the stream
             E.restore_m0();
             E.ret();

@@ -117,6 +117,8 @@ const Knob kKnobs[] = {
     {"TSG_JIT_XDIRECT", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_HALF", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_QBLOCK", "16 | 8", [](const char *v) { return one_of(v, {"16", "8"}); }},
+    {"TSG_JIT_STAGGER", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
+    {"TSG_JIT_PRIO", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_ROWS64_MAXM", "0..65536", [](const char *v) { return int_in(v, 0, 65536); }},
     {"TSG_JIT_NOALIGN", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_GN", "1..1024", [](const char *v) { return int_in(v, 1, 1024); }},

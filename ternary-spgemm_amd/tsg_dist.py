@@ -181,17 +181,22 @@ class GatherPipeline:
     chunking M").
 
         compute(0); ag(0)
-        compute(1); ag(1); wait(0); reorder(0)
+        compute(1); ag(1); [side stream: wait(0); reorder(0)]
         ...
-        wait(C-1); reorder(C-1)
+        [side stream: wait(C-1); reorder(C-1)]; current stream waits for the side stream
 
     `compute(r0, r1, Y_chunk)` must enqueue (GPU) or perform (CPU) Y[r0:r1,
     n0:n1] into the contiguous Y_chunk [r1-r0, w_local] on the current stream;
     the all-gather of a chunk is issued async right after its compute, so the
     collective's stream waits for that compute only and runs beside the next
-    chunk's kernel.  Buffers are allocated once: the gather buffers in
-    __init__, and for an uneven shard (w_local < the widest shard) one
-    contiguous [Mc, w_local] compute buffer per chunk on the first run() --
+    chunk's kernel.  On the GPU the reorder of a gathered chunk ([P, Mc, w]
+    rank-major -> Y_full's rows, one strided copy that moves 2 x 4 Mc N bytes)
+    runs on a side stream behind that chunk's collective, beside the next
+    chunk's compute (the kernel is VALU-bound, the copy HBM-bound); the
+    caller's stream waits for the side stream before run() returns, so the
+    whole step stays ordered on it.  Buffers are allocated once: the gather
+    buffers in __init__, and for an uneven shard (w_local < the widest shard)
+    one contiguous [Mc, w_local] compute buffer per chunk on the first run() --
     no allocation per step."""
 
     def __init__(self, M: int, N: int, world: int, chunks: int = 4, device=None, dtype=None,
@@ -206,6 +211,8 @@ class GatherPipeline:
         self.G = [torch.empty((world * (r1 - r0), self.wmax), dtype=dtype, device=device)
                   for r0, r1 in self.ranges]
         self._narrow = None  # (w_local, [Mc, w_local] buffers) for an uneven shard
+        cuda = torch.device(device).type == "cuda" if device is not None else False
+        self.side = torch.cuda.Stream(device=device) if cuda else None  # the reorders
 
     def _narrow_buffers(self, w_local: int):
         if self._narrow is None or self._narrow[0] != w_local:
@@ -213,9 +220,14 @@ class GatherPipeline:
         return self._narrow[1]
 
     def run(self, compute: Callable, Y_full, w_local: int) -> None:
-        import torch.distributed as dist
+        import torch
         pending = []
         narrow = self._narrow_buffers(w_local) if w_local != self.wmax else None
+        main = torch.cuda.current_stream(Y_full.device) if self.side is not None else None
+        if main is not None:
+            # the side stream's reorders write Y_full and read the gather
+            # buffers: ordered after everything the caller enqueued before
+            self.side.wait_stream(main)
         for i, (r0, r1) in enumerate(self.ranges):
             Yc = self.Yloc[i]
             if narrow is None:
@@ -229,8 +241,20 @@ class GatherPipeline:
                 self._finish(*pending.pop(0), Y_full)
         for p in pending:
             self._finish(*p, Y_full)
+        if main is not None:
+            main.wait_stream(self.side)
 
     def _finish(self, i: int, work, Y_full) -> None:
-        work.wait()
+        import torch
         r0, r1 = self.ranges[i]
-        _reorder(self.G[i].view(self.world, r1 - r0, self.wmax), Y_full[r0:r1], self.widths)
+        if self.side is None:
+            work.wait()
+            _reorder(self.G[i].view(self.world, r1 - r0, self.wmax), Y_full[r0:r1], self.widths)
+            return
+        if isinstance(work, _Done):
+            # gloo with device tensors (the one-GPU rehearsal): the gathered
+            # chunk was copied in on the caller's stream
+            self.side.wait_stream(torch.cuda.current_stream(Y_full.device))
+        with torch.cuda.stream(self.side):
+            work.wait()  # the side stream waits for the collective (RCCL), not the caller's stream
+            _reorder(self.G[i].view(self.world, r1 - r0, self.wmax), Y_full[r0:r1], self.widths)

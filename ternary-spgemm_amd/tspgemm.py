@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
     "tcsc_hip_host_register", "tcsc_hip_host_unregister", "tcsc_hip_set_far", "tcsc_hip_call_far",
     "tsg_jit_codegen_far", "tsg_call_plan", "tsg_knob_check", "tcsc_hip_set_tile_rows", "tcsc_hip_call_tile_rows",
-    "tsg_jit_codegen64", "tsg_jit_codegen64h",
+    "tsg_jit_codegen64", "tsg_jit_codegen64h", "tcsc_hip_call_launches",
 )
 
 
@@ -133,6 +133,7 @@ def lib() -> C.CDLL:
     L.tcsc_hip_set_far.argtypes = [H, C.c_int]
     L.tcsc_hip_set_tile_rows.argtypes = [H, C.c_int]
     L.tcsc_hip_call_tile_rows.argtypes = [H, C.c_int]
+    L.tcsc_hip_call_launches.argtypes = [H, C.c_void_p, C.c_int]
     L.tsg_jit_codegen64.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                     C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tsg_jit_codegen64h.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
@@ -664,6 +665,13 @@ class TCSCDevice:
         """M tile (64 / 128) of the weight-compiled image a call with M rows
         runs; 0 when it runs a small-M walk."""
         return int(lib().tcsc_hip_call_tile_rows(self._h, M))
+
+    def call_launches(self, X, M: int) -> int:
+        """Device kernels a device-pointer call with M rows and this X (a cuda
+        tensor or a device pointer) launches: 1 (the kernel reads X itself) or
+        2 (an X^T staging kernel first)."""
+        ptr = X.data_ptr() if hasattr(X, "data_ptr") else int(X)
+        return int(lib().tcsc_hip_call_launches(self._h, C.c_void_p(ptr), M))
 
     def call_far(self, M: int) -> bool:
         """True if a call with M rows runs the far-X^T image."""

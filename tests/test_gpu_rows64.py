@@ -159,6 +159,9 @@ def test_rows64_direct_x_and_staged(tsg, oracle_mod, monkeypatch, M, K, qblock):
         for shift in (0, 1):  # 0: 16-B aligned (direct when K allows); 1: 4-byte offset (staged)
             X = buf[shift:shift + M * K].view(M, K)
             X.copy_(torch.from_numpy(Xh))
+            if qblock == "rows":  # tcsc_hip_call_launches: 1 when the kernel reads X itself
+                direct_ok = direct == "1" and shift == 0 and K >= 188 and K % 4 == 0
+                assert h.call_launches(X, M) == (1 if direct_ok else 2), (M, K, direct, shift)
             Y = h.gemm_torch(X, b)
             torch.cuda.synchronize()
             assert _bits_eq(Y.cpu().numpy(), ref), (M, K, shift, direct, qblock)

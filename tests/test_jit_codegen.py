@@ -123,6 +123,8 @@ def _decode(code, pc, G):
         return "vadd", (d, x, op == 2), 1
     if (w0 & 0xFFFFFFF0) == 0xBF800000:
         return "nop", (), 1
+    if w0 in (0xBF8F0000, 0xBF8F0001):  # s_setprio 0 / 1 (TSG_JIT_PRIO: issue arbitration only)
+        return "nop", (), 1
     if (w0 & 0xFFFFF0FF) == 0xBF8CC07F:
         return "wait_lgkm", ((w0 >> 8) & 0xF,), 1
     if (w0 & 0xFFFFFFF0) == 0xBF8C0F70:  # s_waitcnt vmcnt(n), n <= 15
@@ -692,3 +694,22 @@ def test_tile_map_is_a_bijection(tsg, gn, gm):
             assert 0 <= nt < ntiles and 0 <= mt < mtiles
             seen.add((nt, mt))
         assert len(seen) == mtiles * ntiles, (mtiles, ntiles, gn, gm)
+
+
+@pytest.mark.parametrize("knobs", [{"TSG_JIT_STAGGER": "1"}, {"TSG_JIT_PRIO": "1"},
+                                   {"TSG_JIT_STAGGER": "1", "TSG_JIT_PRIO": "1"}])
+@pytest.mark.parametrize("M,K,N,s,width,rows64", [(130, 400, 520, 4, 64, False), (70, 500, 1100, 4, 128, True),
+                                                  (64, 1000, 300, 16, 16, True), (5, 97, 40, 2, 8, True),
+                                                  (200, 188, 600, 8, 32, True), (1, 1, 1, 1, 64, True)])
+def test_jit_code_stagger_and_priority(tsg, oracle_mod, monkeypatch, knobs, M, K, N, s, width, rows64):
+    """The stagger (TSG_JIT_STAGGER=1: waves 0-3 run half a step ahead of
+    waves 4-7, their barrier mid-step, their DMA pieces after it) and the
+    static priority (TSG_JIT_PRIO=1: s_setprio 1 for waves 4-7): the emulated
+    workgroup checks every LDS read against landed pieces (no read-after-DMA
+    race) and every DMA against reads since its issue (no write-after-read
+    race), with the barrier counts equal across waves -- and the result equals
+    the oracle bit for bit."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    for frac in (False, True):
+        _check(tsg, oracle_mod, M, K, N, s, 11 + K, frac, width=width, waves=8, rows64=rows64)
