@@ -108,3 +108,25 @@ def test_plan_rejects_bad_arguments(tsg):
         tsg.call_plan(64, 0, 0, 1)
     with pytest.raises(tsg.TSGError):
         tsg.call_plan(64, 64, 64 * 64 + 1, 1)
+
+
+def test_ell_maxm_knob_leaves_small_w_rule():
+    """TSG_ELL_MAXM moves only the small-M boundary; the small-W
+    rule (M x nnz <= 420 M, K in one chunk: the walk up to M = 128) is
+    independent of it -- set to its default the plan is unchanged.  A fresh
+    process: the knob is read once."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    code = ("import sys; sys.path.insert(0, %r); import tspgemm as T; "
+            "print(T.call_plan(2048, 8192, 2048 * 8192 // 8, 64)['kernel'], "
+            "T.call_plan(4096, 16384, 4096 * 16384 // 4, 48)['kernel'])" % (REPO + "/ternary-spgemm_amd"))
+    import os
+    for env_val in (None, "32"):
+        env = dict(os.environ)
+        env.pop("TSG_ELL_MAXM", None)
+        if env_val:
+            env["TSG_ELL_MAXM"] = env_val
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout.split() == ["tsg_tcsc_ell_kernel", "tsg_jit64_kernel"], (env_val, r.stdout)
