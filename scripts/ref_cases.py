@@ -46,9 +46,21 @@ def main():
         b = torch.full((N,), 2.0, device=dev)
         Y = torch.empty((M, N), device=dev)
         h.reserve(M)
-        for _ in range(20):  # warmup incl. the GPU clock ramp
+        import time
+        t_end = time.perf_counter() + 0.2
+        while time.perf_counter() < t_end:  # warmup incl. the GPU clock ramp
+            for _ in range(4):
+                h.gemm_torch(X, b, Y)
+            torch.cuda.synchronize()
+        # the call back to back without per-launch timing events (round 5:
+        # an event pair idles the GPU ~10 us per launch): stream time per call
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.steps):
             h.gemm_torch(X, b, Y)
+        e1.record()
         torch.cuda.synchronize()
+        step_ms = e0.elapsed_time(e1) / a.steps
         h.set_timing(True)
         h.kernel_time(reset=True)
         for _ in range(a.steps):
@@ -63,6 +75,7 @@ def main():
         adds = T.flops(M, N, nnz)
         hbm = T.algorithmic_bytes(M, N, K, nnz)
         print(json.dumps({"M": M, "K": K, "N": N, "s": s, "kernel": h.call_kernel(M), "kernel_ms": round(ms, 4),
+                          "step_ms": round(step_ms, 4), "launches": h.call_launches(X, M),
                           "gflops": round(adds / (ms * 1e-3) / 1e9, 1),
                           "valu_frac": round(adds / (ms * 1e-3) / VALU_PEAK, 4),
                           "hbm_frac": round(hbm / (ms * 1e-3) / HBM_PEAK, 4),
