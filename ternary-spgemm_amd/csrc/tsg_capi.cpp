@@ -549,8 +549,12 @@ void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, i
     // s = 8 / 16 680.6-681.2 / 444.3-448.1 vs 684.7-690.5 / 458.2-462.8 us
     // (r04t_tmask_sparse_ab.txt); (16000, 8192, 2048) s = 4 / 8 1227-1239 /
     // 729-735 vs 1248-1261 / 739-749 us (r04t_tmask_long_ab.txt; (8192, 16384,
-    // 4096) within its run-to-run spread)
-    const bool wide_short = nw == tsg::kJit64WideNW;
+    // 4096) within its run-to-run spread) -- but not for sparse W over long K
+    // (round 5, direct X on the row layout, kernel us, r05p_tmask_long_ab.jsonl):
+    // (64000, 16384, 4096) s = 8 / 16 14640 / 8310 thinned vs 10796 / 7020
+    // with every tile touching, (16000, 8192, 2048) s = 8 / 16 799 / 532 vs
+    // 726 / 494; (8192, 16384, 4096) s = 4 a tie (2359 vs 2355)
+    const bool wide_short = nw == tsg::kJit64WideNW && (h->K < 8192 || density > 0.1875);
     tmask = env_tm >= 0 ? env_tm
                         : (((int64_t)mtiles * ntiles <= kJitOneRoundWgs || wide_short) && mtiles >= 4 ? 3 : 0);
     int n = 2, m = 16;

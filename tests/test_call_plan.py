@@ -25,9 +25,11 @@ import pytest
     # ... s = 2 (code past the Infinity Cache) 128-row on 1 x 32 (r03f_sparse_big_ab.txt; the 64-row
     # image 50.6 vs 39.0 ms, r04m_w128_big.jsonl) ...
     ((64000, 16384, 4096, 2), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
-    # ... s = 8 / 16 on the 64-row image's 128 x 8, 4 x 8 (11.2 / 7.2 vs 14.3 / 8.7 ms, r04m)
-    ((64000, 16384, 4096, 8), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
-    ((64000, 16384, 4096, 16), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
+    # ... s = 8 / 16 on the 64-row image's 128 x 8, 4 x 8 (11.2 / 7.2 vs 14.3 / 8.7 ms, r04m), every
+    # M tile touching its code (10.8 / 7.0 vs 14.6 / 8.3 ms thinned, r05p_tmask_long_ab.jsonl)
+    ((64000, 16384, 4096, 8), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
+    ((64000, 16384, 4096, 16), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
+    ((16000, 8192, 2048, 8), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 8), tmask=0)),
     # X^T too small for the far image (r03e_long_k_ab.txt): 64-row 128 x 8 (2467 vs 2833 us, r04m) / large enough
     ((8192, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
     # (the far image only from X^T >= 2 GiB: at 1 GiB the 64-row 128 x 8 wins, 4.75 vs 5.69 ms, r04p_far_ab.jsonl)
