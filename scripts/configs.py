@@ -18,8 +18,9 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(REPO, "ternary-spgemm_amd"), os.path.join(REPO, "oracle")]
+sys.path[:0] = [os.path.join(REPO, "ternary-spgemm_amd"), os.path.join(REPO, "oracle"), os.path.dirname(os.path.abspath(__file__))]
 import tspgemm as T  # noqa: E402
+from step_timing import time_calls  # noqa: E402
 
 SHAPES = [("configs[0]", 32, 1024, 4096, 4), ("configs[1]", 512, 4096, 4096, 4),
           ("configs[2]", 4096, 4096, 16384, 4),
@@ -61,24 +62,17 @@ def main():
         b = torch.full((N,), 2.0, device=dev)
         Y = torch.empty((M, N), device=dev)
         h.reserve(M)
-        for _ in range(20):  # warmup incl. the GPU clock ramp (profiles/r02c_clock_ramp.txt)
-            h.gemm_torch(X, b, Y)
-        torch.cuda.synchronize()
-        h.set_timing(True)
-        h.kernel_time(reset=True)
-        t1 = time.perf_counter()
-        for _ in range(a.steps):
-            h.gemm_torch(X, b, Y)
-        torch.cuda.synchronize()
-        step_ms = (time.perf_counter() - t1) / a.steps * 1e3
-        ms, n = h.kernel_time(reset=True)
-        ms /= max(n, 1)
+        t = time_calls(h, X, b, Y, a.steps)
+        step_ms = t["step_ms"]
+        # the kernel's duration: stream time per call when the call is one launch
+        ms = step_ms if t["launches"] == 1 else t["event_pair_kernel_ms"]
         rows = min(M, 8)
         ref = O.base_tcsc(X[:rows].cpu().numpy(), O.TCSC(*arrs, K, N), np.full(N, 2.0, np.float32))
         ok = bool(np.array_equal(ref.view(np.uint32), Y[:rows].cpu().numpy().view(np.uint32)))
         adds = T.flops(M, N, nnz)
         print(json.dumps({"shape": name, "M": M, "K": K, "N": N, "s": s, "kernel": h.call_kernel(M),
-                          "kernel_ms": round(ms, 4), "step_ms": round(step_ms, 4),
+                          "kernel_ms": round(ms, 4), "step_ms": round(step_ms, 4), "launches": t["launches"],
+                          "event_pair_kernel_ms": round(t["event_pair_kernel_ms"], 4),
                           "gflops_kernel": round(adds / (ms * 1e-3) / 1e9, 1),
                           "valu_frac": round(adds / (ms * 1e-3) / 78.64e12, 4),
                           "jit_width": jw, "jit_waves": h.jit_waves(M), "width_pinned": bool(width),

@@ -22,8 +22,9 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(REPO, "ternary-spgemm_amd"), os.path.join(REPO, "oracle")]
+sys.path[:0] = [os.path.join(REPO, "ternary-spgemm_amd"), os.path.join(REPO, "oracle"), os.path.dirname(os.path.abspath(__file__))]
 import tspgemm as T  # noqa: E402
+from step_timing import time_calls  # noqa: E402
 
 
 def main():
@@ -67,17 +68,11 @@ def main():
                  else T.TCSCDevice.from_blocked(*blk, K, N, a.B, device=0))
             out[f"{fmt}_register_s"] = round(time.time() - t0, 3)
             h.reserve(M)
-            for _ in range(20):  # warmup incl. the GPU clock ramp (profiles/r02c_clock_ramp.txt)
-                h.gemm_torch(X, b, Y)
-            torch.cuda.synchronize()
-            h.set_timing(True)
-            h.kernel_time(reset=True)
-            for _ in range(a.steps):
-                h.gemm_torch(X, b, Y)
-            torch.cuda.synchronize()
-            ms, n = h.kernel_time(reset=True)
-            h.set_timing(False)
-            ms /= max(n, 1)
+            t = time_calls(h, X, b, Y, a.steps)
+            # the kernel's duration: stream time per call when the call is one launch
+            ms = t["step_ms"] if t["launches"] == 1 else t["event_pair_kernel_ms"]
+            out[f"{fmt}_step_ms"] = round(t["step_ms"], 4)
+            out[f"{fmt}_event_pair_kernel_ms"] = round(t["event_pair_kernel_ms"], 4)
             bb = np.full(N, 2.0, np.float32)
             ref = (O.base_blocked_tcsc(Xs, blk, bb, K, N, a.B) if fmt == "blocked"
                    else O.base_tcsc(Xs, O.TCSC(*arrs, K, N), bb))
