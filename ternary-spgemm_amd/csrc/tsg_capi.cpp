@@ -62,7 +62,7 @@ struct tsg_tcsc {
     int jit_force = 0;                    // tcsc_hip_set_jit_width / TSG_JIT_NW: 0 = auto
     uint32_t *d_status = nullptr;         // jit dispatcher status word (nonzero: region check failed)
     // images that failed to load or probe at a call (bit variant_bit): calls
-    // that pick them run the 128-row 64 x 8 image loaded at registration
+    // that pick them run the 128-row 64 x 8 image (loaded on that fallback)
     uint32_t bad_variants = 0;
     // small-M kernel (tsg_ell.hip): one sliced-ELL image per variant, built on
     // the first call (or tcsc_hip_reserve) that picks the variant
@@ -495,14 +495,14 @@ JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64)
 
 // The image and shape a jit call with M rows runs: the automatic (or pinned)
 // pick, unless that image failed to load at an earlier call -- then the
-// 128-row 64 x 8 image loaded at registration (run_dev's fallback).
-// A call may fall back from an image that cannot be loaded to the registered
-// 128-row 64 x 8 image when nothing pinned its image or shape (a pinned
-// request fails loudly instead: TSG_ERR_HIP).
+// 128-row 64 x 8 image (run_dev's fallback, which loads it).
+// A call may fall back from an image that cannot be loaded to the 128-row
+// 64 x 8 image when nothing pinned its image or shape (a pinned request fails
+// loudly instead: TSG_ERR_HIP).
 bool may_fall_back(const tsg_tcsc *h, const JitShape &sh)
 {
     const bool is_default = !sh.r64 && !sh.far && sh.nw == tsg::kJitNW && sh.waves == tsg::kJitWaves;
-    return !is_default && !h->tile_rows && !h->jit_force && h->far_mode != 2 && h->jv[0].mod.function &&
+    return !is_default && !h->tile_rows && !h->jit_force && h->far_mode != 2 &&
            !tsg::knob_value("TSG_JIT_ROWS64_MAXM") && !tsg::knob_value("TSG_JIT_NW");
 }
 
@@ -847,12 +847,14 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         rc = ensure_jit_variant(h, sh.nw, sh.waves, s, sh.far, sh.r64, sh.half);
         if (rc == TSG_ERR_HIP && may_fall_back(h, sh)) {
             // an image the loader refuses (or whose probe fails): this and later
-            // calls that pick it run the 128-row 64 x 8 image registered at
-            // tcsc_hip_create -- same result bit for bit, another speed
+            // calls that pick it run the 128-row 64 x 8 image -- same result
+            // bit for bit, another speed
             std::fprintf(stderr, "[ternary_spgemm] warning: %s; running the 128-row 64 x 8 image instead\n",
                          g_tsg_host_err.c_str());
             h->bad_variants |= 1u << variant_bit(sh);
             sh = JitShape{tsg::kJitNW, tsg::kJitWaves};
+            rc = ensure_jit_variant(h, sh.nw, sh.waves, s);
+            if (rc) return rc;
         } else if (rc) {
             return rc;
         }
@@ -1248,7 +1250,16 @@ int create_impl(const int32_t *csp, const int32_t *csn, const int32_t *rip, cons
             }
             h->jit_force = nw;
         }
-        const int rc0 = ensure_jit_variant(h, h->jit_force ? h->jit_force : tsg::kJitNW);
+        // Registration compiles, loads and probes the image most calls run --
+        // the 64-row image's 128 x 8 (configs[2] and the sparse end, M >= 1024
+        // at N = 16384) -- so a handle does not also carry the 128-row image
+        // (8 B per nonzero) unless a call picks it or falls back to it.  If the
+        // 64-row image cannot load here, the 128-row 64 x 8 one is tried (calls
+        // that pick a 64-row image then warn and fall back, run_dev), then rx.
+        h->jit_nch = std::max(1, (K + tsg::kJitChunk - 1) / tsg::kJitChunk);
+        int rc0 = !B && !h->jit_force && !tsg::knob_value("TSG_JIT_ROWS64_MAXM") ? ensure_jit_variant(h, tsg::kJit64WideNW, tsg::kJitWaves, nullptr, false, true)
+                                                                                 : TSG_ERR_ARG;
+        if (rc0) rc0 = ensure_jit_variant(h, h->jit_force ? h->jit_force : tsg::kJitNW);
         if (rc0) {
             // A generated image that the loader refuses (or whose probe launch
             // does not find its region) falls back to the rx kernel, unless jit
@@ -1406,7 +1417,7 @@ extern "C" int tcsc_hip_reserve(tsg_tcsc *h, int max_M)
                 std::fprintf(stderr, "[ternary_spgemm] warning: %s; running the 128-row 64 x 8 image instead\n",
                              g_tsg_host_err.c_str());
                 h->bad_variants |= 1u << variant_bit(sh);
-                rc = TSG_OK;
+                rc = ensure_jit_variant(h, tsg::kJitNW);
             }
             if (rc) return rc;
         }
