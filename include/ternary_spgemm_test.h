@@ -122,11 +122,14 @@ int tsg_jit_tile_map(int L, int mtiles, int ntiles, int gn, int gm, int *nt, int
 /* The small-M kernel's sliced-ELL image for an M tile of MT rows and K chunks
  * of at most Cmax rows (tsg_ell.hip header): entry words (2 uint16 LDS float
  * indices each) and per (16-column slice, step) {offset in 256-B units,
- * 8-entry blocks}; *C, *nch: chunk rows and chunks.  Host only; NULL buffers
- * query the lengths (in uint32). */
+ * 8-entry blocks}; *C, *nch: chunk rows and chunks.  copies = 2 (MT = 8
+ * only; 1 otherwise): two X^T copies in LDS, the second at float *xb, each
+ * entry pointing at one of them (tsg_internal.h ell_copy_offset); *xb = 0
+ * with one copy.  Host only; NULL buffers query the lengths (in uint32). */
 int tsg_ell_build(const int32_t *col_start_pos, const int32_t *col_start_neg, const int32_t *row_index_pos,
-                  const int32_t *row_index_neg, int K, int N, int Cmax, int MT, uint32_t *ent, int64_t ent_cap,
-                  int64_t *ent_len, uint32_t *tab, int64_t tab_cap, int64_t *tab_len, int32_t *C, int32_t *nch);
+                  const int32_t *row_index_neg, int K, int N, int Cmax, int MT, int copies, uint32_t *ent,
+                  int64_t ent_cap, int64_t *ent_len, uint32_t *tab, int64_t tab_cap, int64_t *tab_len, int32_t *C,
+                  int32_t *nch, int32_t *xb);
 
 /* The 64-row image (no reference counterpart): one M row per
  * lane, 64-row M tiles, every nonzero one 4-byte VOP2 v_add_f32 / v_sub_f32,

@@ -174,7 +174,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t n)
 // are +0.
 template <int MT, int NT, int SB>
 __device__ __forceinline__ void ell_stage(float *xs, const float *__restrict__ X, int M, int K, int m0, int kc, int C,
-                                          int tid, bool vec)
+                                          int tid, bool vec, int xb)
 {
     const int per = C / 4 * MT;
     if (vec) {
@@ -198,6 +198,12 @@ __device__ __forceinline__ void ell_stage(float *xs, const float *__restrict__ X
                     xs[(r4 + 1) * MT + mm] = w.y;
                     xs[(r4 + 2) * MT + mm] = w.z;
                     xs[(r4 + 3) * MT + mm] = w.w;
+                    if (xb) {  // the second copy (tsg_host.cpp build_ell_image)
+                        xs[xb + (r4 + 0) * MT + mm] = w.x;
+                        xs[xb + (r4 + 1) * MT + mm] = w.y;
+                        xs[xb + (r4 + 2) * MT + mm] = w.z;
+                        xs[xb + (r4 + 3) * MT + mm] = w.w;
+                    }
                 }
             }
         }
@@ -216,6 +222,12 @@ __device__ __forceinline__ void ell_stage(float *xs, const float *__restrict__ X
             xs[(r4 + 1) * MT + mm] = w.y;
             xs[(r4 + 2) * MT + mm] = w.z;
             xs[(r4 + 3) * MT + mm] = w.w;
+            if (xb) {
+                xs[xb + (r4 + 0) * MT + mm] = w.x;
+                xs[xb + (r4 + 1) * MT + mm] = w.y;
+                xs[xb + (r4 + 2) * MT + mm] = w.z;
+                xs[xb + (r4 + 3) * MT + mm] = w.w;
+            }
         }
     }
 }
@@ -226,7 +238,7 @@ template <int LG, int RPL, int WPG, int LA, bool PRELU>
 __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
     const float *__restrict__ X, const uint4 *__restrict__ ent, const uint2 *__restrict__ tab,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N, int K,
-    int C, int nch, int steps, int nsg)
+    int C, int nch, int steps, int nsg, int xb)
 {
     constexpr int MT = LG * RPL;                     // M rows of the tile
     constexpr int CPW = 64 / LG;                     // columns per wave
@@ -248,8 +260,11 @@ __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
 #pragma unroll
     for (int r = 0; r < RPL; r++) y[r] = 0.0f;  // comp.h:41
 
-    // the zero row (padding entries point at it)
-    for (int i = tid; i < MT; i += WPG * 64) xs[C * MT + i] = 0.0f;
+    // the zero row (padding entries point at it); and the second copy's
+    for (int i = tid; i < MT; i += WPG * 64) {
+        xs[C * MT + i] = 0.0f;
+        if (xb) xs[xb + C * MT + i] = 0.0f;
+    }
 
     for (int step = 0; step < steps; step++) {
         // the step's entry stream first: its blocks travel while X is staged
@@ -276,7 +291,7 @@ __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
         const int j = steps == 1 ? 0 : step % nch, kc = j * C;
         if (step == 0 || steps > 1) {
             __syncthreads();  // previous chunk's reads are done
-            ell_stage<MT, WPG * 64, SB>(xs, X, M, K, m0, kc, C, tid, vec);
+            ell_stage<MT, WPG * 64, SB>(xs, X, M, K, m0, kc, C, tid, vec, xb);
             __syncthreads();
         }
         ell_walk<RPL, D, LA>(y, q, e0, off, n8, n8pos, nmax, base);
@@ -382,7 +397,7 @@ __global__ __launch_bounds__(64 * (MT + E / 8)) void tsg_tcsc_ell_pc_kernel(
     }
     for (int i = tid; i < MT; i += S::NT) xs[C * MT + i] = 0.0f;  // the zero row
     const bool vec = K >= 4 && (K & 3) == 0 && ((((uintptr_t)X) & 15) == 0);
-    ell_stage<MT, S::NT, 8>(xs, X, M, K, m0, 0, C, tid, vec);
+    ell_stage<MT, S::NT, 8>(xs, X, M, K, m0, 0, C, tid, vec, 0);
     lds_barrier();
 
     if (consumer) {
@@ -515,20 +530,20 @@ namespace {
 
 template <int LG, int RPL, int WPG, int LA>
 int launch_ell_la(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
-                  int M, int N, int K, int C, int nch, int prelu, hipStream_t s)
+                  int M, int N, int K, int C, int nch, int xb, int prelu, hipStream_t s)
 {
     constexpr int MT = LG * RPL, CPW = 64 / LG;
     const int nsg = (N + WPG * CPW - 1) / (WPG * CPW);
     const int mtiles = (M + MT - 1) / MT;
     const int steps = nch == 1 ? 1 : 2 * nch;
-    const size_t lds = (size_t)(C + 1) * MT * sizeof(float);
+    const size_t lds = ell_lds_floats(C, MT, xb) * sizeof(float);
     const dim3 grid((unsigned)(nsg * mtiles)), block(WPG * 64);
     if (prelu)
         hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, LA, true>), grid, block, lds, s, X, ent, tab, b, alpha,
-                           Y, M, N, K, C, nch, steps, nsg);
+                           Y, M, N, K, C, nch, steps, nsg, xb);
     else
         hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, LA, false>), grid, block, lds, s, X, ent, tab, b, alpha,
-                           Y, M, N, K, C, nch, steps, nsg);
+                           Y, M, N, K, C, nch, steps, nsg, xb);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -545,34 +560,54 @@ int pick_la()
 
 template <int LG, int RPL, int WPG>
 int launch_ell_t(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
-                 int M, int N, int K, int C, int nch, int prelu, hipStream_t s)
+                 int M, int N, int K, int C, int nch, int xb, int prelu, hipStream_t s)
 {
-    if (pick_la() == 2) return launch_ell_la<LG, RPL, WPG, 2>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, prelu, s);
-    return launch_ell_la<LG, RPL, WPG, 1>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, prelu, s);
+    if (pick_la() == 2) return launch_ell_la<LG, RPL, WPG, 2>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+    return launch_ell_la<LG, RPL, WPG, 1>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
 }
 
 }  // namespace
 
 namespace {
 
-// Waves per workgroup: the fewest (4, 8, 16) that keep every wave resident in
-// one round, given the workgroups per CU the LDS chunk allows (a workgroup
-// stages its chunk once for all its columns); 8 and 16 only while a lane holds
-// at most 2 rows (more spill at 8 and 16 waves).
+// Waves per workgroup: 16 or 8 when the grid still gives (nearly) every CU a
+// workgroup (waves >= kEllWideWgs x WPG) -- a workgroup stages its X chunk once for
+// all its columns, so fewer, wider workgroups stage less (round 5,
+// profiles/r05t_ell_wpg_ab.jsonl, kernel us: (32, 2048, 8192) 21.2 vs 29.0 at
+// 4 waves; (16, 2048, 16384) 21.1 vs 29.7; (32, 2048, 16384) 31.2 vs 38.2 at
+// 4, 37.9 at 8), else the fewest (4, 8, 16) that keep every wave resident in
+// one round, given the workgroups per CU the LDS chunk allows ((16, 1024,
+// 4096) 11.7 at 4 vs 13.6 at 8); 8 and 16 only while a lane holds at most 2
+// rows (more spill at 8 and 16 waves).  TSG_ELL_WPG=4/8/16 forces one (A/B).
+constexpr int64_t kEllWideWgs = 224;  // 7/8 of the CUs
+
 template <int LG, int RPL>
 int launch_lg(const float *X, const uint4 *e, const uint2 *t, const float *b, const float *alpha, float *Y, int M,
-              int N, int K, int C, int nch, int prelu, hipStream_t s)
+              int N, int K, int C, int nch, int xb, int prelu, hipStream_t s)
 {
     constexpr int MT = LG * RPL, CPW = 64 / LG;
     const int64_t waves = (int64_t)((N + CPW - 1) / CPW) * ((M + MT - 1) / MT);
-    const int64_t per_cu = std::max<int64_t>(1, 163840 / ((int64_t)(C + 1) * MT * 4));
+    const int64_t per_cu = std::max<int64_t>(1, 163840 / ((int64_t)ell_lds_floats(C, MT, xb) * 4));
+    static const int env_wpg = [] {  // TSG_ELL_WPG=4/8/16: waves per workgroup (A/B)
+        const char *v = knob_value("TSG_ELL_WPG");
+        return v ? atoi(v) : 0;
+    }();
+    if (env_wpg == 4) return launch_ell_t<LG, RPL, 4>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
     if constexpr (RPL <= 2) {
-        if (waves > 256 * per_cu * 8)
-            return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, prelu, s);
-        if (waves > 256 * per_cu * 4)
-            return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, prelu, s);
+        if (env_wpg == 8) return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        if (env_wpg == 16) return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
     }
-    return launch_ell_t<LG, RPL, 4>(X, e, t, b, alpha, Y, M, N, K, C, nch, prelu, s);
+    if constexpr (RPL <= 2) {
+        if (waves >= kEllWideWgs * 16)
+            return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        if (waves >= kEllWideWgs * 8)
+            return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        if (waves > 256 * per_cu * 8)
+            return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        if (waves > 256 * per_cu * 4)
+            return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+    }
+    return launch_ell_t<LG, RPL, 4>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
 }
 
 // lanes per column of an M tile: the default, or TSG_ELL_LG (diagnostic sweeps)
@@ -663,15 +698,17 @@ int launch_tcsc_ell_pc(int variant, const float *X, const uint32_t *ent, const u
 }
 
 int launch_tcsc_ell(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
-                    const float *alpha, float *Y, int M, int N, int K, int C, int nch, int prelu, void *stream)
+                    const float *alpha, float *Y, int M, int N, int K, int C, int nch, int xb, int prelu, void *stream)
 {
+    // the second X^T copy serves the 8-row tile's 4-lane columns only (tsg_host.cpp build_ell_image)
+    if (xb && (variant != 2 || pick_lg(4) != 4)) return -2;
     hipStream_t s = (hipStream_t)stream;
     const uint4 *e = reinterpret_cast<const uint4 *>(ent);
     const uint2 *t = reinterpret_cast<const uint2 *>(tab);
 #define TSG_ELL_LG(lg, rpl) \
-    case lg: return launch_lg<lg, rpl>(X, e, t, b, alpha, Y, M, N, K, C, nch, prelu, s)
+    case lg: return launch_lg<lg, rpl>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s)
     switch (variant) {
-    case 0: return launch_ell_t<1, 1, 1>(X, e, t, b, alpha, Y, M, N, K, C, nch, prelu, s);  // MT = 1
+    case 0: return launch_ell_t<1, 1, 1>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);  // MT = 1
     case 1:                                                                                   // MT = 4
         switch (pick_lg(4)) {
             TSG_ELL_LG(4, 1);

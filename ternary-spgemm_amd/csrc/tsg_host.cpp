@@ -90,13 +90,23 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 // {offset in blocks, n8 | n8pos << 16}: the first n8pos blocks add, the rest
 // subtract.  Block 0 is all padding (the walk reads it past a list's end).
 void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
-                     int Cmax, int MT, EllImage &img)
+                     int Cmax, int MT, EllImage &img, int copies)
 {
-    img.C = std::min(Cmax, std::max(4, (K + 3) / 4 * 4));
+    const bool two = copies == 2 && MT == 8;
+    if (two) {
+        // both copies (and their zero rows) inside the LDS: xb + (C + 1) * MT
+        // floats <= kLdsBytes / 4, chunks balanced over K
+        const int cmax2 = std::min(Cmax, ((int)(kLdsBytes / 4) - 96) / (2 * MT) - 1) / 4 * 4;
+        const int nch2 = std::max(1, (K + cmax2 - 1) / cmax2);
+        img.C = std::max(4, ((K + nch2 - 1) / nch2 + 3) / 4 * 4);
+    } else {
+        img.C = std::min(Cmax, std::max(4, (K + 3) / 4 * 4));
+    }
     img.nch = std::max(1, (K + img.C - 1) / img.C);
     img.steps = img.nch == 1 ? 1 : 2 * img.nch;
     img.nslices = (N + 15) / 16;
-    const int C = img.C, nch = img.nch, steps = img.steps;
+    img.xb = two ? ell_copy_offset(img.C, MT) : 0;
+    const int C = img.C, nch = img.nch, steps = img.steps, xb = img.xb;
     const uint16_t pad = (uint16_t)(C * MT);
     img.tab.assign((size_t)img.nslices * steps * 2, 0u);
     std::vector<uint16_t> e16((size_t)128, pad);  // block 0: the padding block
@@ -136,6 +146,39 @@ void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                         e16[base + (size_t)(i / 8) * 128 + (size_t)c * 8 + (size_t)(i % 8)] = (uint16_t)((k - j * C) * MT);
                     }
                     cur[p][c] += cnt[c];
+                }
+                if (two) {
+                    // per entry position (block, entry) and ds_read_b64 lane
+                    // group (columns 0-7, 8-15): each entry reads copy A or B,
+                    // whichever window (8 banks: float index % 64 / 8) holds
+                    // fewer distinct rows of the group so far (greedy; a row
+                    // already there broadcasts)
+                    for (int i8 = 0; i8 < b8; i8++)
+                        for (int h = 0; h < 8; h++)
+                            for (int g0 = 0; g0 < 16; g0 += 8) {
+                                int nwin[8] = {0};
+                                uint32_t seen[8][8];
+                                for (int c = g0; c < g0 + 8; c++) {
+                                    uint16_t &u = e16[base + (size_t)i8 * 128 + (size_t)c * 8 + (size_t)h];
+                                    const uint32_t cand[2] = {u, (uint32_t)(xb + u)};
+                                    int best = 0, best_load = 1 << 30;
+                                    for (int o = 0; o < 2; o++) {
+                                        const int w = (int)(cand[o] % 64 / 8);
+                                        bool dup = false;
+                                        for (int t = 0; t < nwin[w]; t++) dup |= seen[w][t] == cand[o];
+                                        const int load = dup ? nwin[w] : nwin[w] + 1;
+                                        if (load < best_load) {
+                                            best_load = load;
+                                            best = o;
+                                        }
+                                    }
+                                    const int w = (int)(cand[best] % 64 / 8);
+                                    bool dup = false;
+                                    for (int t = 0; t < nwin[w]; t++) dup |= seen[w][t] == cand[best];
+                                    if (!dup) seen[w][nwin[w]++] = cand[best];
+                                    u = (uint16_t)cand[best];
+                                }
+                            }
                 }
                 n8 += (uint32_t)b8;
                 if (p == 0) n8pos = (uint32_t)b8;
@@ -423,8 +466,8 @@ extern "C" int tsg_csc_packed_to_tcsc(const int32_t *col_ptr, const int32_t *row
 // Host-only view of the small-M kernel's sliced-ELL image (tests decode it and
 // replay the kernel's walk on the CPU).  NULL buffers query the lengths.
 extern "C" int tsg_ell_build(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K,
-                             int N, int Cmax, int MT, uint32_t *ent, int64_t ent_cap, int64_t *ent_len, uint32_t *tab,
-                             int64_t tab_cap, int64_t *tab_len, int32_t *C, int32_t *nch)
+                             int N, int Cmax, int MT, int copies, uint32_t *ent, int64_t ent_cap, int64_t *ent_len,
+                             uint32_t *tab, int64_t tab_cap, int64_t *tab_len, int32_t *C, int32_t *nch, int32_t *xb)
 {
     const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N);
     if (!e.empty() || Cmax < 4 || Cmax % 4 || MT < 1 || (int64_t)Cmax * MT >= 65536) {
@@ -432,8 +475,13 @@ extern "C" int tsg_ell_build(const int32_t *csp, const int32_t *csn, const int32
                                    : "tsg_ell_build: " + e;
         return TSG_ERR_ARG;
     }
+    if (copies != 1 && copies != 2) {
+        g_tsg_host_err = "tsg_ell_build: copies must be 1 or 2";
+        return TSG_ERR_ARG;
+    }
     tsg::EllImage img;
-    tsg::build_ell_image(csp, csn, rip, rin, K, N, Cmax, MT, img);
+    tsg::build_ell_image(csp, csn, rip, rin, K, N, Cmax, MT, img, copies);
+    if (xb) *xb = img.xb;
     if (ent_len) *ent_len = (int64_t)img.ent.size();
     if (tab_len) *tab_len = (int64_t)img.tab.size();
     if (C) *C = img.C;

@@ -151,8 +151,9 @@ def lib() -> C.CDLL:
     L.tcsc_hip_call_kernel.restype = C.c_char_p
     L.tsg_knob_check.argtypes = []
     L.tsg_knob_check.restype = C.c_char_p
-    L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.POINTER(C.c_int64),
-                                vp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.tsg_ell_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
+                                C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     L.tsg_jit_tile_map.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.tcsc_hip_jit_width.argtypes = [H, C.c_int]
     L.tcsc_hip_jit_waves.argtypes = [H, C.c_int]
@@ -336,20 +337,23 @@ def jit_tile_map(L: int, mtiles: int, ntiles: int, gn: int, gm: int):
     return nt.value, mt.value
 
 
-def ell_build(csp, csn, rip, rin, K: int, N: int, Cmax: int, MT: int):
+def ell_build(csp, csn, rip, rin, K: int, N: int, Cmax: int, MT: int, copies: int = 1, with_xb: bool = False):
     """Host view of the small-M kernel's sliced-ELL image for an M tile of MT
     rows (tsg_ell.hip): (entries uint16[] = LDS float indices, tab
-    uint32[slices*steps, 2], C, nch)."""
+    uint32[slices*steps, 2], C, nch), and the second X^T copy's float offset
+    xb when with_xb (copies=2: MT = 8 only, tsg_internal.h ell_copy_offset)."""
     csp, csn, rip, rin = _i32(csp), _i32(csn), _i32(rip), _i32(rin)
-    ne, nt, c, nch = C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32()
+    ne, nt, c, nch, xb = C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32(), C.c_int32()
     L = lib()
-    _check(L.tsg_ell_build(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, Cmax, MT, None, 0, C.byref(ne), None, 0,
-                           C.byref(nt), C.byref(c), C.byref(nch)), "tsg_ell_build")
+    _check(L.tsg_ell_build(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, Cmax, MT, copies, None, 0, C.byref(ne),
+                           None, 0, C.byref(nt), C.byref(c), C.byref(nch), C.byref(xb)), "tsg_ell_build")
     ent = np.empty(ne.value, np.uint32)
     tab = np.empty(nt.value, np.uint32)
-    _check(L.tsg_ell_build(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, Cmax, MT, _ptr(ent), ne.value,
-                           C.byref(ne), _ptr(tab), nt.value, C.byref(nt), C.byref(c), C.byref(nch)), "tsg_ell_build")
-    return ent.view(np.uint16), tab.reshape(-1, 2), c.value, nch.value
+    _check(L.tsg_ell_build(_ptr(csp), _ptr(csn), _ptr(rip), _ptr(rin), K, N, Cmax, MT, copies, _ptr(ent), ne.value,
+                           C.byref(ne), _ptr(tab), nt.value, C.byref(nt), C.byref(c), C.byref(nch), C.byref(xb)),
+           "tsg_ell_build")
+    out = (ent.view(np.uint16), tab.reshape(-1, 2), c.value, nch.value)
+    return out + (xb.value,) if with_xb else out
 
 
 def tcsc_to_blocked(csp, csn, rip, rin, K: int, N: int, B: int):

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 
-def replay(ent, tab, C, nch, X, K, N, MT):
+def replay(ent, tab, C, nch, X, K, N, MT, xb=0):
     M = X.shape[0]
     steps = 1 if nch == 1 else 2 * nch
     nslices = (N + 15) // 16
@@ -34,6 +34,8 @@ def replay(ent, tab, C, nch, X, K, N, MT):
                 for i in range(n8):
                     for u in blk[i, c, :]:
                         u = int(u)
+                        if xb and u >= xb:  # the second X^T copy (same rows)
+                            u -= xb
                         assert u % MT == 0 and u // MT <= C
                         x = xs[u // MT]
                         y[:, col] = y[:, col] + x if i < n8pos else y[:, col] - x
@@ -67,3 +69,44 @@ def test_ell_rejects_bad_chunk(tsg, oracle_mod):
         tsg.ell_build(*t.arrays, 64, 20, 6, 4)
     with pytest.raises(tsg.TSGError):
         tsg.ell_build(*t.arrays, 64, 20, 4096, 16)  # indices past 16 bits
+
+
+def _window_loads(ent, tab, xb):
+    """max over 8-bank windows of the distinct rows a ds_read_b64 lane group
+    (8 columns x 4 lanes of 2 rows) reads, per entry position: the LDS cycles
+    of that group (MI355X_MICROARCH.md LDS: bank = float index % 64)"""
+    loads = []
+    for off, w in tab:
+        n8 = int(w) & 0xFFFF
+        blk = ent[int(off) * 128:(int(off) + n8) * 128].reshape(n8, 16, 8).astype(np.int64)
+        for i in range(n8):
+            for h in range(8):
+                for g0 in (0, 8):
+                    addrs = set(int(a) for a in blk[i, g0:g0 + 8, h])
+                    win = {}
+                    for a in addrs:
+                        win[a % 64 // 8] = win.get(a % 64 // 8, 0) + 1
+                    loads.append(max(win.values()))
+    return np.array(loads)
+
+
+@pytest.mark.parametrize("M,K,N,s", [(8, 1024, 64, 4), (5, 3000, 48, 4), (3, 700, 33, 2)])
+def test_ell_two_copies(tsg, oracle_mod, M, K, N, s):
+    """Round 5: the 8-row tile's image with two X^T copies (TSG_ELL_COPIES=2):
+    same results bit for bit, both copies and the zero rows inside the LDS,
+    and the copy choice lowers the lane groups' bank-window loads."""
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(K, N, s, M + K + N))
+    ent, tab, C, nch, xb = tsg.ell_build(*t.arrays, K, N, 5116, 8, copies=2, with_xb=True)
+    assert xb % 64 == 32 and xb >= (C + 1) * 8 and xb + (C + 1) * 8 <= 40960 and C % 4 == 0
+    b = np.linspace(-1, 2, N).astype(np.float32)
+    for X in (O.init_x_int(M, K, 3), O.init_x_frac(M, K, 4)):
+        Y = replay(ent, tab, C, nch, X, K, N, 8, xb) + b
+        assert np.array_equal(Y.view(np.uint32), O.base_tcsc(X, t, b).view(np.uint32))
+    e1, t1, C1, nch1 = tsg.ell_build(*t.arrays, K, N, C, 8)  # one copy, same chunks
+    assert (C1, nch1) == (C, nch)
+    two, one = _window_loads(ent, tab, xb), _window_loads(e1, t1, 0)
+    assert len(two) == len(one) and two.sum() < one.sum() and two.max() <= one.max()
+    assert ent.max() < xb + (C + 1) * 8
+    with pytest.raises(tsg.TSGError):
+        tsg.ell_build(*t.arrays, K, N, 5116, 8, copies=3)
