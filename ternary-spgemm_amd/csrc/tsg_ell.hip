@@ -570,8 +570,10 @@ int launch_ell_t(const float *X, const uint4 *ent, const uint2 *tab, const float
 
 namespace {
 
-// Waves per workgroup: 16 or 8 when the grid still gives (nearly) every CU a
-// workgroup (waves >= kEllWideWgs x WPG) -- a workgroup stages its X chunk once for
+// Waves per workgroup: 16 or 8 when the grid is then one round that still
+// gives (nearly) every CU a workgroup (kEllWideWgs ... 256 x the workgroups
+// per CU the LDS chunk allows; (24, 4096, 16384) at 8 waves would take two
+// rounds: 60.8 vs 52.5 us at 16) -- a workgroup stages its X chunk once for
 // all its columns, so fewer, wider workgroups stage less (round 5,
 // profiles/r05t_ell_wpg_ab.jsonl, kernel us: (32, 2048, 8192) 21.2 vs 29.0 at
 // 4 waves; (16, 2048, 16384) 21.1 vs 29.7; (32, 2048, 16384) 31.2 vs 38.2 at
@@ -598,10 +600,12 @@ int launch_lg(const float *X, const uint4 *e, const uint2 *t, const float *b, co
         if (env_wpg == 16) return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
     }
     if constexpr (RPL <= 2) {
-        if (waves >= kEllWideWgs * 16)
-            return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
-        if (waves >= kEllWideWgs * 8)
-            return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        auto one_round = [&](int64_t wpg) {  // >= 7/8 of the CUs busy, no second round
+            const int64_t wgs = (waves + wpg - 1) / wpg;
+            return wgs >= kEllWideWgs && wgs <= 256 * per_cu;
+        };
+        if (one_round(16)) return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        if (one_round(8)) return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
         if (waves > 256 * per_cu * 8)
             return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
         if (waves > 256 * per_cu * 4)
