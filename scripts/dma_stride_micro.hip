@@ -16,11 +16,12 @@
 #include <cstdlib>
 
 constexpr int kBuf = 48 * 1024;
+constexpr int kBufA = 49 * 1024;  // ring buffer pitch (49 pieces for the aligned row runs)
 
 __global__ __launch_bounds__(512, 1) void stage(const char *__restrict__ x, int mode, int pr, uint32_t ld,
                                                int nch, int steps, int mtiles, uint32_t *sink)
 {
-    __shared__ __attribute__((aligned(16))) char lds[3 * kBuf];
+    __shared__ __attribute__((aligned(16))) char lds[3 * kBufA];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int mt = blockIdx.x % mtiles;
@@ -28,7 +29,8 @@ __global__ __launch_bounds__(512, 1) void stage(const char *__restrict__ x, int 
     for (int q = 0; q < steps; q++) {
         const int c = q % nch, buf = q % 3;
 #pragma unroll
-        for (int i = 0; i < 6; i++) {
+        for (int i = 0; i < 7; i++) {
+            if (i == 6 && mode != 3) continue;
             const int p = wave * 6 + i;
             uint64_t off;
             if (mode == 0) {  // staged copy: piece (c, mt, p) = 1 KiB contiguous
@@ -37,6 +39,13 @@ __global__ __launch_bounds__(512, 1) void stage(const char *__restrict__ x, int 
                 if (p >= 47) continue;
                 const int slot = p * 64 + lane, row = mt * 64 + slot / 47, quad = slot % 47;
                 off = (uint64_t)row * ld + (uint64_t)c * 752 + quad * 16;
+            } else if (mode == 3) {  // aligned row runs: 48 quads (768 B = 12 lines) per row from
+                // 64-B aligned chunk starts, LDS rows of 49 quads (the 49th a pad: its lane
+                // re-reads the row's last quad); 49 pieces per chunk (6 or 7 per wave)
+                if (i == 6 && wave >= 1) continue;  // 8 waves x 6 + wave 0's 7th = 49 pieces
+                const int pp = i == 6 ? 48 : p;
+                const int slot = pp * 64 + lane, row = mt * 64 + slot / 49, q = slot % 49, quad = q < 48 ? q : 47;
+                off = (uint64_t)row * ld + (uint64_t)c * 768 + quad * 16;
             } else {  // direct: PR rows x (64 / PR) quads of row-major X
                 const int rgs = 64 / pr;
                 const int row = mt * 64 + (p % rgs) * pr + lane % pr;
@@ -44,7 +53,8 @@ __global__ __launch_bounds__(512, 1) void stage(const char *__restrict__ x, int 
                 off = (uint64_t)row * ld + (uint64_t)c * 768 + quad * 16;
             }
             const char *g = x + off;
-            const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(buf * kBuf + p * 1024));
+            const int pl = mode == 3 && i == 6 ? 48 : p;  // LDS piece slot
+            const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(buf * kBufA + pl * 1024));
             asm volatile("s_mov_b32 m0, %0\n\t"
                          "s_nop 0\n\t"
                          "global_load_lds_dwordx4 %1, off"
@@ -85,7 +95,8 @@ int main(int argc, char **argv)
                  {"direct PR=8,  pitch K*4+128", 1, 8, 128},
                  {"direct PR=8,  pitch K*4+256", 1, 8, 256},
                  {"row runs (47-quad rows), pitch K*4", 2, 0, 0},
-                 {"row runs (47-quad rows), pitch K*4+256", 2, 0, 256}};
+                 {"row runs (47-quad rows), pitch K*4+256", 2, 0, 256},
+                 {"aligned row runs (48 of 49 quads)", 3, 0, 0}};
     printf("M=%d K=%d grid=%d mtiles=%d chunks=%d steps=%d (48 KiB per step per workgroup)\n", M, K, grid, mtiles, nch,
            steps);
     for (int rep = 0; rep < 2; rep++)
