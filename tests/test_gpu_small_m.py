@@ -141,6 +141,24 @@ def test_config3_shape_small_m(tsg, oracle_mod, M):
     h.close()
 
 
+@pytest.mark.parametrize("M,K,N", [(16, 2048, 8192), (32, 2048, 8192), (16, 2048, 16384), (24, 2048, 16384),
+                                   (32, 2048, 16384), (24, 4096, 16384)])
+def test_walk_workgroup_shapes_full_y(tsg, oracle_mod, M, K, N):
+    """Round 5's waves-per-workgroup rule (tsg_ell.hip launch_lg): these
+    shapes run the walk with 4, 8 and 16 waves per workgroup, in one round or
+    more; every element against the oracle with order-sensitive X."""
+    import torch
+    O = oracle_mod
+    arrs = tsg.gen_tcsc(K, N, 4, 7)
+    h = tsg.TCSCDevice(*arrs, K, N)
+    assert h.call_kernel(M) == "tsg_tcsc_ell_kernel"
+    Xn = O.init_x_frac(M, K, 11)
+    b = np.linspace(-2, 2, N).astype(np.float32)
+    Y = h.gemm_torch(torch.from_numpy(Xn).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+    assert _bits_eq(Y, O.base_tcsc(Xn, O.TCSC(*arrs, K, N), b, threads=16))
+    h.close()
+
+
 def test_config0_runs_small_m(tsg, oracle_mod):
     """configs[0] (M = 32, K = 1024, N = 4096, s = 4; BASELINE.json) takes the
     small-M kernel automatically (8-row tiles; 12 us vs 26 us on the jit
