@@ -156,9 +156,11 @@ typedef struct tsg_info {
     int64_t tcsc_bytes;     /* TCSC::getDataStructureSize() (TCSC.h:43-49) */
     int64_t image_bytes;    /* bytes of the device image (segments + entries) */
     int64_t work_bytes;     /* current work-buffer size */
-    int32_t chunk_rows;     /* K rows per LDS chunk of the device image */
-    int32_t tile_rows;      /* M rows per workgroup */
-    int32_t tile_cols;      /* N columns per workgroup */
+    int32_t chunk_rows;     /* K rows per LDS chunk of the image registration loaded
+                               (the 64-row image's 128 x 8 shape when it could, else the
+                               128-row image's 64 x 8, or rx); calls may compile others */
+    int32_t tile_rows;      /* M rows per workgroup (same image) */
+    int32_t tile_cols;      /* N columns per workgroup (same image) */
     int32_t reserved;
 } tsg_info;
 int tcsc_hip_info(const tsg_tcsc *h, tsg_info *out);

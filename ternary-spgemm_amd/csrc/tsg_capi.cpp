@@ -1668,9 +1668,13 @@ extern "C" int tcsc_hip_info(const tsg_tcsc *h, tsg_info *o)
     for (const auto &e : h->ell) jit_bytes += e.bytes;
     o->image_bytes = jit ? jit_bytes : (int64_t)(h->rimg.wstart.size() + h->rimg.ent.size()) * 4;
     o->work_bytes = (int64_t)h->work_bytes;
-    o->chunk_rows = jit ? tsg::kJitChunk : tsg::kRxChunk;
-    o->tile_rows = jit ? tsg::kJitTileM : tsg::kRxTileM;
-    o->tile_cols = jit ? tsg::kJitTileCols : tsg::kRxTileCols;
+    // the image registration loaded: the 64-row image's 128 x 8 when it could
+    // (create_impl), else the 128-row 64 x 8 one (or rx)
+    const tsg_tcsc::JitVariant &r64 = h->jv64[shape_index(tsg::kJit64WideNW, tsg::kJitWaves, false)];
+    const bool reg64 = jit && r64.mod.function;
+    o->chunk_rows = reg64 ? r64.chunk : jit ? tsg::kJitChunk : tsg::kRxChunk;
+    o->tile_rows = reg64 ? tsg::kJit64TileM : jit ? tsg::kJitTileM : tsg::kRxTileM;
+    o->tile_cols = reg64 ? tsg::kJit64WideNW * tsg::kJitWaves : jit ? tsg::kJitTileCols : tsg::kRxTileCols;
     return TSG_OK;
 }
 

@@ -16,6 +16,8 @@ def test_four_kernels_on_one_handle(tsg, oracle_mod):
     K, N, s = 700, 300, 4
     t = O.tcsc_encode(O.gen_ternary(K, N, s, 1234))
     h = tsg.TCSCDevice(*t.arrays, K, N, device=0)
+    info = h.info()  # the registration image: the 64-row image's 128 x 8
+    assert (info["tile_rows"], info["tile_cols"], info["chunk_rows"]) == (64, 1024, 188)
     b = np.linspace(-3, 3, N).astype(np.float32)
     ran = []
     for M in (600, 96, 5, 1):
