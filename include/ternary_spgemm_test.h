@@ -125,7 +125,9 @@ int tsg_jit_tile_map(int L, int mtiles, int ntiles, int gn, int gm, int *nt, int
  * 8-entry blocks}; *C, *nch: chunk rows and chunks.  copies = 2 (MT = 8
  * only; 1 otherwise): two X^T copies in LDS, the second at float *xb, each
  * entry pointing at one of them (tsg_internal.h ell_copy_offset); *xb = 0
- * with one copy.  Host only; NULL buffers query the lengths (in uint32). */
+ * with one copy.  copies = 3 (MT = 8): one copy with the bank-window schedule
+ * (tsg_internal.h kEllSchedZeroRows), *xb = minus its zero rows after the
+ * chunk.  Host only; NULL buffers query the lengths (in uint32). */
 int tsg_ell_build(const int32_t *col_start_pos, const int32_t *col_start_neg, const int32_t *row_index_pos,
                   const int32_t *row_index_neg, int K, int N, int Cmax, int MT, int copies, uint32_t *ent,
                   int64_t ent_cap, int64_t *ent_len, uint32_t *tab, int64_t tab_cap, int64_t *tab_len, int32_t *C,

@@ -771,13 +771,25 @@ int ell_copies(int v)
     return v == kEllTile8 ? env : 1;
 }
 
+// The bank-window schedule of the 8-row tile's image (tsg_internal.h
+// kEllSchedZeroRows): TSG_ELL_SCHED=0 / 1 (A/B)
+bool ell_sched(int v)
+{
+    static const int env = [] {
+        const char *c = tsg::knob_value("TSG_ELL_SCHED");
+        const char *lg = tsg::knob_value("TSG_ELL_LG");
+        return c && c[0] == '1' && (!lg || std::atoi(lg) == 4) ? 1 : 0;
+    }();
+    return v == kEllTile8 && env && ell_copies(v) == 1;
+}
+
 int ensure_ell(tsg_tcsc *h, int v)
 {
     tsg_tcsc::EllVariant &e = h->ell[v];
     if (e.ready) return TSG_OK;
     tsg::build_ell_image(h->csp.data(), h->csn.data(), h->rip.empty() ? nullptr : h->rip.data(),
                          h->rin.empty() ? nullptr : h->rin.data(), h->K, h->N, tsg::kEllMaxC[v], tsg::kEllTileM[v], e.img,
-                         ell_copies(v));
+                         ell_copies(v), ell_sched(v));
     DeviceGuard g(h->device);
     const size_t eb = e.img.ent.size() * 4, tb = std::max<size_t>(e.img.tab.size() * 4, 8);
     // allocate and upload into locals; the variant owns them only once both
@@ -842,7 +854,7 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
         const int lrc = use_ell_pc(h, ev) ? tsg::launch_tcsc_ell_pc(ev, dX, e.d_ent, e.d_tab, db, dalpha, dY, M, N, K,
                                                                     e.img.C, e.img.nch, prelu ? 1 : 0, s)
                                           : tsg::launch_tcsc_ell(ev, dX, e.d_ent, e.d_tab, db, dalpha, dY, M, N, K,
-                                                                 e.img.C, e.img.nch, e.img.xb, prelu ? 1 : 0, s);
+                                                                 e.img.C, e.img.nch, e.img.xb, e.img.zr, prelu ? 1 : 0, s);
         if (lrc != 0)
             return fail(TSG_ERR_HIP, std::string("small-M kernel launch: ") + hipGetErrorString(hipGetLastError()));
         if (slot >= 0) {

@@ -238,7 +238,7 @@ template <int LG, int RPL, int WPG, int LA, bool PRELU>
 __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
     const float *__restrict__ X, const uint4 *__restrict__ ent, const uint2 *__restrict__ tab,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N, int K,
-    int C, int nch, int steps, int nsg, int xb)
+    int C, int nch, int steps, int nsg, int xb, int zr)
 {
     constexpr int MT = LG * RPL;                     // M rows of the tile
     constexpr int CPW = 64 / LG;                     // columns per wave
@@ -261,9 +261,9 @@ __global__ __launch_bounds__(WPG * 64) void tsg_tcsc_ell_kernel(
     for (int r = 0; r < RPL; r++) y[r] = 0.0f;  // comp.h:41
 
     // the zero row (padding entries point at it); and the second copy's
-    for (int i = tid; i < MT; i += WPG * 64) {
+    for (int i = tid; i < zr * MT; i += WPG * 64) {
         xs[C * MT + i] = 0.0f;
-        if (xb) xs[xb + C * MT + i] = 0.0f;
+        if (xb && i < MT) xs[xb + C * MT + i] = 0.0f;
     }
 
     for (int step = 0; step < steps; step++) {
@@ -530,20 +530,20 @@ namespace {
 
 template <int LG, int RPL, int WPG, int LA>
 int launch_ell_la(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
-                  int M, int N, int K, int C, int nch, int xb, int prelu, hipStream_t s)
+                  int M, int N, int K, int C, int nch, int xb, int zr, int prelu, hipStream_t s)
 {
     constexpr int MT = LG * RPL, CPW = 64 / LG;
     const int nsg = (N + WPG * CPW - 1) / (WPG * CPW);
     const int mtiles = (M + MT - 1) / MT;
     const int steps = nch == 1 ? 1 : 2 * nch;
-    const size_t lds = ell_lds_floats(C, MT, xb) * sizeof(float);
+    const size_t lds = ell_lds_floats(C, MT, xb, zr) * sizeof(float);
     const dim3 grid((unsigned)(nsg * mtiles)), block(WPG * 64);
     if (prelu)
         hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, LA, true>), grid, block, lds, s, X, ent, tab, b, alpha,
-                           Y, M, N, K, C, nch, steps, nsg, xb);
+                           Y, M, N, K, C, nch, steps, nsg, xb, zr);
     else
         hipLaunchKernelGGL((tsg_tcsc_ell_kernel<LG, RPL, WPG, LA, false>), grid, block, lds, s, X, ent, tab, b, alpha,
-                           Y, M, N, K, C, nch, steps, nsg, xb);
+                           Y, M, N, K, C, nch, steps, nsg, xb, zr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -560,10 +560,11 @@ int pick_la()
 
 template <int LG, int RPL, int WPG>
 int launch_ell_t(const float *X, const uint4 *ent, const uint2 *tab, const float *b, const float *alpha, float *Y,
-                 int M, int N, int K, int C, int nch, int xb, int prelu, hipStream_t s)
+                 int M, int N, int K, int C, int nch, int xb, int zr, int prelu, hipStream_t s)
 {
-    if (pick_la() == 2) return launch_ell_la<LG, RPL, WPG, 2>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
-    return launch_ell_la<LG, RPL, WPG, 1>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+    if (pick_la() == 2)
+        return launch_ell_la<LG, RPL, WPG, 2>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
+    return launch_ell_la<LG, RPL, WPG, 1>(X, ent, tab, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
 }
 
 }  // namespace
@@ -585,33 +586,33 @@ constexpr int64_t kEllWideWgs = 224;  // 7/8 of the CUs
 
 template <int LG, int RPL>
 int launch_lg(const float *X, const uint4 *e, const uint2 *t, const float *b, const float *alpha, float *Y, int M,
-              int N, int K, int C, int nch, int xb, int prelu, hipStream_t s)
+              int N, int K, int C, int nch, int xb, int zr, int prelu, hipStream_t s)
 {
     constexpr int MT = LG * RPL, CPW = 64 / LG;
     const int64_t waves = (int64_t)((N + CPW - 1) / CPW) * ((M + MT - 1) / MT);
-    const int64_t per_cu = std::max<int64_t>(1, 163840 / ((int64_t)ell_lds_floats(C, MT, xb) * 4));
+    const int64_t per_cu = std::max<int64_t>(1, 163840 / ((int64_t)ell_lds_floats(C, MT, xb, zr) * 4));
     static const int env_wpg = [] {  // TSG_ELL_WPG=4/8/16: waves per workgroup (A/B)
         const char *v = knob_value("TSG_ELL_WPG");
         return v ? atoi(v) : 0;
     }();
-    if (env_wpg == 4) return launch_ell_t<LG, RPL, 4>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+    if (env_wpg == 4) return launch_ell_t<LG, RPL, 4>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
     if constexpr (RPL <= 2) {
-        if (env_wpg == 8) return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
-        if (env_wpg == 16) return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        if (env_wpg == 8) return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
+        if (env_wpg == 16) return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
     }
     if constexpr (RPL <= 2) {
         auto one_round = [&](int64_t wpg) {  // >= 7/8 of the CUs busy, no second round
             const int64_t wgs = (waves + wpg - 1) / wpg;
             return wgs >= kEllWideWgs && wgs <= 256 * per_cu;
         };
-        if (one_round(16)) return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
-        if (one_round(8)) return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+        if (one_round(16)) return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
+        if (one_round(8)) return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
         if (waves > 256 * per_cu * 8)
-            return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+            return launch_ell_t<LG, RPL, 16>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
         if (waves > 256 * per_cu * 4)
-            return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+            return launch_ell_t<LG, RPL, 8>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
     }
-    return launch_ell_t<LG, RPL, 4>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);
+    return launch_ell_t<LG, RPL, 4>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);
 }
 
 // lanes per column of an M tile: the default, or TSG_ELL_LG (diagnostic sweeps)
@@ -702,17 +703,19 @@ int launch_tcsc_ell_pc(int variant, const float *X, const uint32_t *ent, const u
 }
 
 int launch_tcsc_ell(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
-                    const float *alpha, float *Y, int M, int N, int K, int C, int nch, int xb, int prelu, void *stream)
+                    const float *alpha, float *Y, int M, int N, int K, int C, int nch, int xb, int zr, int prelu,
+                    void *stream)
 {
-    // the second X^T copy serves the 8-row tile's 4-lane columns only (tsg_host.cpp build_ell_image)
-    if (xb && (variant != 2 || pick_lg(4) != 4)) return -2;
+    // the second X^T copy and the bank-window schedule serve the 8-row tile's
+    // 4-lane columns only (tsg_host.cpp build_ell_image)
+    if ((xb || zr != 1) && (variant != 2 || pick_lg(4) != 4)) return -2;
     hipStream_t s = (hipStream_t)stream;
     const uint4 *e = reinterpret_cast<const uint4 *>(ent);
     const uint2 *t = reinterpret_cast<const uint2 *>(tab);
 #define TSG_ELL_LG(lg, rpl) \
-    case lg: return launch_lg<lg, rpl>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s)
+    case lg: return launch_lg<lg, rpl>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s)
     switch (variant) {
-    case 0: return launch_ell_t<1, 1, 1>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, prelu, s);  // MT = 1
+    case 0: return launch_ell_t<1, 1, 1>(X, e, t, b, alpha, Y, M, N, K, C, nch, xb, zr, prelu, s);  // MT = 1
     case 1:                                                                                   // MT = 4
         switch (pick_lg(4)) {
             TSG_ELL_LG(4, 1);

@@ -90,18 +90,24 @@ void build_rx_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
 // {offset in blocks, n8 | n8pos << 16}: the first n8pos blocks add, the rest
 // subtract.  Block 0 is all padding (the walk reads it past a list's end).
 void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
-                     int Cmax, int MT, EllImage &img, int copies)
+                     int Cmax, int MT, EllImage &img, int copies, bool sched)
 {
     const bool two = copies == 2 && MT == 8;
+    sched = sched && MT == 8 && !two;
     if (two) {
         // both copies (and their zero rows) inside the LDS: xb + (C + 1) * MT
         // floats <= kLdsBytes / 4, chunks balanced over K
         const int cmax2 = std::min(Cmax, ((int)(kLdsBytes / 4) - 96) / (2 * MT) - 1) / 4 * 4;
         const int nch2 = std::max(1, (K + cmax2 - 1) / cmax2);
         img.C = std::max(4, ((K + nch2 - 1) / nch2 + 3) / 4 * 4);
+    } else if (sched) {
+        // the chunk and its 8 zero rows inside the LDS
+        img.C = std::min(std::min(Cmax, (int)(kLdsBytes / 4) / MT - kEllSchedZeroRows) / 4 * 4,
+                         std::max(4, (K + 3) / 4 * 4));
     } else {
         img.C = std::min(Cmax, std::max(4, (K + 3) / 4 * 4));
     }
+    img.zr = sched ? kEllSchedZeroRows : 1;
     img.nch = std::max(1, (K + img.C - 1) / img.C);
     img.steps = img.nch == 1 ? 1 : 2 * img.nch;
     img.nslices = (N + 15) / 16;
@@ -137,13 +143,58 @@ void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip,
                     cnt[c] = q - cur[p][c];
                     L = std::max(L, cnt[c]);
                 }
+                std::vector<uint16_t> seq[16];  // sched: each column's entries per position
+                if (sched) {
+                    // per ds_read_b64 lane group (columns 0-7, 8-15) and position:
+                    // the columns with most entries left first, each advancing if
+                    // its next row's 8-bank window (float index % 64 / 8) is still
+                    // free; the rest read the zero row of a free window (one row
+                    // for all of them: a broadcast)
+                    L = 0;
+                    for (int g0 = 0; g0 < 16; g0 += 8) {
+                        int at[8] = {0};
+                        for (;;) {
+                            int order[8], no = 0;
+                            for (int c = 0; c < 8; c++)
+                                if (at[c] < cnt[g0 + c]) order[no++] = c;
+                            if (no == 0) break;
+                            std::stable_sort(order, order + no, [&](int a, int b) {
+                                return cnt[g0 + a] - at[a] > cnt[g0 + b] - at[b];
+                            });
+                            unsigned used = 0, moved = 0;
+                            for (int o = 0; o < no; o++) {
+                                const int c = order[o];
+                                const int k = ri[cur[p][g0 + c] + at[c]];
+                                const uint16_t a = (uint16_t)((k - j * C) * MT);
+                                const int w = a % 64 / 8;
+                                if ((used >> w) & 1u) continue;
+                                used |= 1u << w;
+                                moved |= 1u << c;
+                                seq[g0 + c].push_back(a);
+                                at[c]++;
+                            }
+                            int wz = 0;
+                            while (wz < 8 && ((used >> wz) & 1u)) wz++;
+                            const uint16_t z = (uint16_t)((C + (wz - C % 8 + 8) % 8) * MT);  // zero row in window wz
+                            for (int c = 0; c < 8; c++)
+                                if (!((moved >> c) & 1u)) seq[g0 + c].push_back(z);
+                        }
+                        L = std::max(L, (int)seq[g0].size());
+                    }
+                }
                 const int b8 = (L + 7) / 8;
                 const size_t base = e16.size();
                 e16.resize(base + (size_t)b8 * 128, pad);
                 for (int c = 0; c < 16; c++) {
-                    for (int i = 0; i < cnt[c]; i++) {
-                        const int k = ri[cur[p][c] + i];
-                        e16[base + (size_t)(i / 8) * 128 + (size_t)c * 8 + (size_t)(i % 8)] = (uint16_t)((k - j * C) * MT);
+                    if (sched) {
+                        for (size_t i = 0; i < seq[c].size(); i++)
+                            e16[base + (i / 8) * 128 + (size_t)c * 8 + i % 8] = seq[c][i];
+                    } else {
+                        for (int i = 0; i < cnt[c]; i++) {
+                            const int k = ri[cur[p][c] + i];
+                            e16[base + (size_t)(i / 8) * 128 + (size_t)c * 8 + (size_t)(i % 8)] =
+                                (uint16_t)((k - j * C) * MT);
+                        }
                     }
                     cur[p][c] += cnt[c];
                 }
@@ -469,6 +520,9 @@ extern "C" int tsg_ell_build(const int32_t *csp, const int32_t *csn, const int32
                              int N, int Cmax, int MT, int copies, uint32_t *ent, int64_t ent_cap, int64_t *ent_len,
                              uint32_t *tab, int64_t tab_cap, int64_t *tab_len, int32_t *C, int32_t *nch, int32_t *xb)
 {
+    // copies: 1 or 2 X^T copies; 3 = one copy with the bank-window schedule
+    const bool sched = copies == 3;
+    if (sched) copies = 1;
     const std::string e = tsg::validate_tcsc(csp, csn, rip, rin, K, N);
     if (!e.empty() || Cmax < 4 || Cmax % 4 || MT < 1 || (int64_t)Cmax * MT >= 65536) {
         g_tsg_host_err = e.empty() ? "tsg_ell_build: Cmax must be a multiple of 4 with Cmax * MT < 65536"
@@ -476,12 +530,12 @@ extern "C" int tsg_ell_build(const int32_t *csp, const int32_t *csn, const int32
         return TSG_ERR_ARG;
     }
     if (copies != 1 && copies != 2) {
-        g_tsg_host_err = "tsg_ell_build: copies must be 1 or 2";
+        g_tsg_host_err = "tsg_ell_build: copies must be 1, 2 or 3 (the schedule)";
         return TSG_ERR_ARG;
     }
     tsg::EllImage img;
-    tsg::build_ell_image(csp, csn, rip, rin, K, N, Cmax, MT, img, copies);
-    if (xb) *xb = img.xb;
+    tsg::build_ell_image(csp, csn, rip, rin, K, N, Cmax, MT, img, copies, sched);
+    if (xb) *xb = sched ? -img.zr : img.xb;  // (the schedule: minus its zero rows)
     if (ent_len) *ent_len = (int64_t)img.ent.size();
     if (tab_len) *tab_len = (int64_t)img.tab.size();
     if (C) *C = img.C;

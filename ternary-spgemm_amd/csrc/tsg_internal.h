@@ -238,6 +238,7 @@ constexpr int kEllMaxC[kEllVariants] = {40956, 10236, 5116, 2556, 1276};
 struct EllImage {
     int C = 0, nch = 0, steps = 0, nslices = 0;
     int xb = 0;                  // float offset of the second X^T copy (0: one copy)
+    int zr = 1;                  // zero rows after the chunk (8: the bank-window schedule)
     std::vector<uint32_t> ent;   // uint16 entries, 2 per word (256-B blocks)
     std::vector<uint32_t> tab;   // per (slice, step): {offset in 256-B units, 8-entry blocks}
 };
@@ -249,11 +250,22 @@ struct EllImage {
 // LDS floats of a chunk of C rows (+ the zero row) of an MT-row tile: one copy,
 // or copy B at xb (a multiple of 64 floats + 32 past copy A)
 constexpr int ell_copy_offset(int C, int MT) { return ((C + 1) * MT + 63) / 64 * 64 + 32; }
-__host__ __device__ constexpr int ell_lds_floats(int C, int MT, int xb) { return xb ? xb + (C + 1) * MT : (C + 1) * MT; }
+__host__ __device__ constexpr int ell_lds_floats(int C, int MT, int xb, int zr = 1)
+{
+    return xb ? xb + (C + 1) * MT : (C + zr) * MT;
+}
+// Bank-window schedule (round 5, the 8-row tile's 4-lane columns): per
+// ds_read_b64 lane group of 8 columns and entry position, only columns whose
+// next row lies in a window no other column of the group reads there advance;
+// the others read a zero row (8 of them after the chunk, one per window; all
+// such pads of a position read the same one), so every gather is
+// conflict-free, at ~1.5x the positions (tsg_host.cpp build_ell_image)
+constexpr int kEllSchedZeroRows = 8;
 void build_ell_image(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin, int K, int N,
-                     int Cmax, int MT, EllImage &img, int copies = 1);
+                     int Cmax, int MT, EllImage &img, int copies = 1, bool sched = false);
 int launch_tcsc_ell(int variant, const float *X, const uint32_t *ent, const uint32_t *tab, const float *b,
-                    const float *alpha, float *Y, int M, int N, int K, int C, int nch, int xb, int prelu, void *stream);
+                    const float *alpha, float *Y, int M, int N, int K, int C, int nch, int xb, int zr, int prelu,
+                    void *stream);
 // the producer/consumer walk (tsg_tcsc_ell_pc_kernel) of variant 0 (M = 1) when
 // K fits one chunk and the chunk plus its LDS ring fit kLdsBytes
 // (ell_pc_lds_bytes; 0 = no such variant); -2 = not available for this image

@@ -138,6 +138,7 @@ const Knob kKnobs[] = {
     {"TSG_ELL_PC_E", "16 | 32 | 64", [](const char *v) { return one_of(v, {"16", "32", "64"}); }},
     {"TSG_ELL_COPIES", "1 | 2", [](const char *v) { return one_of(v, {"1", "2"}); }},
     {"TSG_ELL_WPG", "4 | 8 | 16", [](const char *v) { return one_of(v, {"4", "8", "16"}); }},
+    {"TSG_ELL_SCHED", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
 #ifdef TSG_DIAG
     {"TSG_JIT_DIAG", "nobar,nodma,notouch,nolgkm,noreads,novm,samecode,samewave,pairwave", diag_ok},
 #endif

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 
-def replay(ent, tab, C, nch, X, K, N, MT, xb=0):
+def replay(ent, tab, C, nch, X, K, N, MT, xb=0, zr=1):
     M = X.shape[0]
     steps = 1 if nch == 1 else 2 * nch
     nslices = (N + 15) // 16
@@ -18,7 +18,7 @@ def replay(ent, tab, C, nch, X, K, N, MT, xb=0):
     y = np.zeros((M, nslices * 16), np.float32)
     for st in range(steps):
         j = 0 if steps == 1 else st % nch
-        xs = np.zeros((C + 1, M), np.float32)  # X^T chunk + the zero row
+        xs = np.zeros((C + zr, M), np.float32)  # X^T chunk + the zero row(s)
         rows = min(C, K - j * C)
         if rows > 0:
             xs[:rows] = X[:, j * C:j * C + rows].T
@@ -36,7 +36,7 @@ def replay(ent, tab, C, nch, X, K, N, MT, xb=0):
                         u = int(u)
                         if xb and u >= xb:  # the second X^T copy (same rows)
                             u -= xb
-                        assert u % MT == 0 and u // MT <= C
+                        assert u % MT == 0 and u // MT < C + zr
                         x = xs[u // MT]
                         y[:, col] = y[:, col] + x if i < n8pos else y[:, col] - x
     return y[:, :N]
@@ -109,4 +109,25 @@ def test_ell_two_copies(tsg, oracle_mod, M, K, N, s):
     assert len(two) == len(one) and two.sum() < one.sum() and two.max() <= one.max()
     assert ent.max() < xb + (C + 1) * 8
     with pytest.raises(tsg.TSGError):
-        tsg.ell_build(*t.arrays, K, N, 5116, 8, copies=3)
+        tsg.ell_build(*t.arrays, K, N, 5116, 8, copies=4)
+
+
+@pytest.mark.parametrize("M,K,N,s", [(8, 1024, 64, 4), (5, 3000, 48, 4), (3, 700, 33, 2), (2, 5200, 40, 8)])
+def test_ell_bank_window_schedule(tsg, oracle_mod, M, K, N, s):
+    """Round 5: the 8-row tile's image with the bank-window schedule
+    (TSG_ELL_SCHED=1): bit for bit the BaseTCSC chains (pads read one of the
+    8 zero rows), every lane group's gather conflict-free (one distinct row
+    per 8-bank window), every nonzero exactly once, and the chunk plus its
+    zero rows inside the LDS."""
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(K, N, s, M + K + N))
+    ent, tab, C, nch, xb = tsg.ell_build(*t.arrays, K, N, 5116, 8, copies=3, with_xb=True)
+    zr = -xb
+    assert zr == 8 and (C + zr) * 8 * 4 <= 160 * 1024 and C % 4 == 0
+    b = np.linspace(-1, 2, N).astype(np.float32)
+    for X in (O.init_x_int(M, K, 3), O.init_x_frac(M, K, 4)):
+        Y = replay(ent, tab, C, nch, X, K, N, 8, 0, zr) + b
+        assert np.array_equal(Y.view(np.uint32), O.base_tcsc(X, t, b).view(np.uint32))
+    assert _window_loads(ent, tab, 0).max() == 1
+    used = ent[128:int((tab[:, 0] + (tab[:, 1] & 0xFFFF)).max(initial=1)) * 128]
+    assert np.count_nonzero(used < C * 8) == len(t.arrays[2]) + len(t.arrays[3])
