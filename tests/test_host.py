@@ -182,6 +182,7 @@ def _small_tcsc(oracle_mod):
     ("TSG_JIT_QBLOCK", "4", "expected"),
     ("TSG_ELL_COPIES", "3", "expected"),
     ("TSG_ELL_WPG", "12", "expected"),
+    ("TSG_ELL_SCHED", "yes", "expected"),
 ])
 def test_registration_refuses_bad_knobs(tsg, oracle_mod, monkeypatch, var, val, msg):
     """A set knob outside its accepted values -- and, in the product library,
@@ -202,7 +203,7 @@ def test_registration_refuses_bad_knobs(tsg, oracle_mod, monkeypatch, var, val, 
     ("TSG_JIT_DMA", "0.25,1"), ("TSG_JIT_DMA", "0,0,2"), ("TSG_JIT_TOUCH", "1,2"), ("TSG_JIT_READS", "6,12"),
     ("TSG_JIT_CP", "20000,0"), ("TSG_JIT_NOALIGN", "1"), ("TSG_KERNEL", "rx"), ("TSG_ELL_LG", "8"),
     ("TSG_JIT_HALF", "1"), ("TSG_JIT_XDIRECT", "1"), ("TSG_JIT_QBLOCK", "8"), ("TSG_ELL_COPIES", "2"),
-    ("TSG_ELL_WPG", "16"),
+    ("TSG_ELL_WPG", "16"), ("TSG_ELL_SCHED", "1"),
 ])
 def test_accepted_knobs_pass(tsg, monkeypatch, var, val):
     monkeypatch.setenv(var, val)
