@@ -128,7 +128,7 @@ constexpr int64_t kJitFullWgs = 230;
 constexpr int64_t kJitOneRoundWgs = 256;  // one jit workgroup per CU (144 KiB of LDS)
 constexpr double kFarXtBytes = 768.0 * 1024 * 1024;  // X^T >= 3x the 256 MiB Infinity Cache
 constexpr double kFarCodeBytes = 160.0 * 1024 * 1024;  // code image well inside it
-constexpr double kFarKeepXtBytes = 2048.0 * 1024 * 1024;  // X^T >= 8x it: the far image beats the 64-row one
+constexpr double kFarKeepXtBytes = 1536.0 * 1024 * 1024;  // X^T >= 6x it: the far image beats the 64-row one
 constexpr double kXDirectMinAddsPerRow = 32.0;  // 64-row image: direct X from width x density >= this
 constexpr int64_t kEllStarvedWgs = 64;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
@@ -378,10 +378,12 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     if (env_max >= 0) return M <= env_max;
     if (M <= kRows64AutoMaxM) return true;
     const JitShape s = pick_jit_shape(h, M, false);
-    // the far-X^T image (128-row only) where X^T is >= 8x the Infinity Cache:
+    // the far-X^T image (128-row only) where X^T is >= 6x the Infinity Cache:
     // (64000, 16384, 4096) 22.1 vs 24.3 ms for the 64-row 128 x 8, while at
     // (16000, 16384, 4096) the 64-row image wins, 4.75 vs 5.69 ms
-    // (profiles/r04p_far_ab.jsonl; the crossover between them is unmeasured)
+    // (profiles/r04p_far_ab.jsonl); round 5 with direct X on the row layout
+    // (r05z_big_images_ab.jsonl, step ms): (64000, ...) 23.4 vs 26.2, (32000,
+    // ...) -- X^T 1.95 GiB -- 11.9 vs 12.5, (16000, ...) 5.96 vs 5.23
     if (s.far && 4.0 * (double)M * (double)h->K >= kFarKeepXtBytes) return false;
     // dense W over long K: the 128-row image's long-stream map keeps each
     // XCD on one column tile's code ((64000, 16384, 4096) s = 2: 39.0 vs

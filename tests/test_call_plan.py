@@ -32,7 +32,9 @@ import pytest
     ((16000, 8192, 2048, 8), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 8), tmask=0)),
     # X^T too small for the far image (r03e_long_k_ab.txt): 64-row 128 x 8 (2467 vs 2833 us, r04m) / large enough
     ((8192, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
-    # (the far image only from X^T >= 2 GiB: at 1 GiB the 64-row 128 x 8 wins, 4.75 vs 5.69 ms, r04p_far_ab.jsonl)
+    # (the far image only from X^T >= 1.5 GiB: at 1 GiB the 64-row 128 x 8 wins, 4.75 vs 5.69 ms, r04p_far_ab.jsonl;
+    # at 1.95 GiB the far image, 11.9 vs 12.5 ms step, r05z_big_images_ab.jsonl)
+    ((32000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
     ((16000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
     # the 64-row image at mid M (round 4, r04d_rows64_ab.jsonl): one round of workgroups,
     # the shape of least modelled time (tsg_capi.cpp pick_jit_shape)
