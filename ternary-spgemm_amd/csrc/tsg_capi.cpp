@@ -385,11 +385,16 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     // (r05z_big_images_ab.jsonl, step ms): (64000, ...) 23.4 vs 26.2, (32000,
     // ...) -- X^T 1.95 GiB -- 11.9 vs 12.5, (16000, ...) 5.96 vs 5.23
     if (s.far && 4.0 * (double)M * (double)h->K >= kFarKeepXtBytes) return false;
-    // dense W over long K: the 128-row image's long-stream map keeps each
-    // XCD on one column tile's code ((64000, 16384, 4096) s = 2: 39.0 vs
-    // 50.6 ms, profiles/r04m_w128_big.jsonl)
+    // dense W over long K and few columns: the 128-row image's long-stream map
+    // keeps each XCD on one column tile's code ((64000, 16384, 4096) s = 2:
+    // 39.0 vs 50.6 ms, profiles/r04m_w128_big.jsonl; round 5, step us,
+    // r05z_dense_longk_ab.jsonl: (4096 / 8192, 16384, 4096) 2442 / 4967 vs
+    // 2518 / 5696); at K = 8192 or N = 16384 the 64-row image with direct X
+    // wins: (16000, 8192, 2048) 2398 vs 2556, (1024, 8192, 4096) 400 vs 428,
+    // (2048, 8192, 1024) 238 vs 341, (2048, 16384, 16384) 4939 vs 5250,
+    // (4096, 8192, 4096) a tie
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
-    if (h->K >= 8192 && density > 0.375) return false;
+    if (h->K >= 16384 && h->N <= 8192 && density > 0.375) return false;
     // 128 columns per wave fill whole rounds: twice the adds per staged chunk
     // and per X read of either 64-wide stream (profiles/r04l_w128_ab.jsonl,
     // r04m_w128_big.jsonl) -- for sparse W or long K, and for dense W over

@@ -35,6 +35,13 @@ import pytest
     # (the far image only from X^T >= 1.5 GiB: at 1 GiB the 64-row 128 x 8 wins, 4.75 vs 5.69 ms, r04p_far_ab.jsonl;
     # at 1.95 GiB the far image, 11.9 vs 12.5 ms step, r05z_big_images_ab.jsonl)
     ((32000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
+    # dense W (s = 2) over long K: the 128-row image only for K >= 16384 with N <= 8192
+    # (r05z_dense_longk_ab.jsonl, step us: (8192, 16384, 4096) 4967 vs 5696); else the 64-row one
+    # ((16000, 8192, 2048) 2398 vs 2556, (2048, 8192, 1024) 238 vs 341, (2048, 16384, 16384) 4939 vs 5250)
+    ((8192, 16384, 4096, 2), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
+    ((16000, 8192, 2048, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 8), tmask=3)),
+    ((2048, 8192, 1024, 2), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(1, 32), tmask=3)),
+    ((2048, 16384, 16384, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
     ((16000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
     # the 64-row image at mid M (round 4, r04d_rows64_ab.jsonl): one round of workgroups,
     # the shape of least modelled time (tsg_capi.cpp pick_jit_shape)
