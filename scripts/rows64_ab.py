@@ -43,9 +43,11 @@ def timed(M, X, Y):
     """kernel ms (HIP events around every launch) and step ms (back-to-back
     calls with the per-kernel events OFF: the events themselves add ~8-10 us
     between launches, profiles/r05g_event_overhead.jsonl)"""
-    for _ in range(20):  # clock warm-up + warmup
-        h.gemm_torch(X, b, Y)
-    torch.cuda.synchronize()
+    t_end = time.perf_counter() + 0.3  # clock warm-up (time-based: 20 calls left the first mode of a process
+    while time.perf_counter() < t_end:  # 3-10% slow, profiles/r05z_r64_shapes_ab.jsonl)
+        for _ in range(4):
+            h.gemm_torch(X, b, Y)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.reps):
         h.gemm_torch(X, b, Y)

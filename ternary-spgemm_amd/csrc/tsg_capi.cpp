@@ -388,10 +388,10 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     // dense W over long K and few columns: the 128-row image's long-stream map
     // keeps each XCD on one column tile's code ((64000, 16384, 4096) s = 2:
     // 39.0 vs 50.6 ms, profiles/r04m_w128_big.jsonl; round 5, step us,
-    // r05z_dense_longk_ab.jsonl: (4096 / 8192, 16384, 4096) 2442 / 4967 vs
-    // 2518 / 5696); at K = 8192 or N = 16384 the 64-row image with direct X
-    // wins: (16000, 8192, 2048) 2398 vs 2556, (1024, 8192, 4096) 400 vs 428,
-    // (2048, 8192, 1024) 238 vs 341, (2048, 16384, 16384) 4939 vs 5250,
+    // r05z_dense_longk2_ab.jsonl: (4096 / 8192, 16384, 4096) 2420 / 4967 vs
+    // 2507 / 5696); at K = 8192 or N = 16384 the 64-row image with direct X
+    // wins: (16000, 8192, 2048) 2393 vs 2546, (1024, 8192, 4096) 366 vs 395,
+    // (2048, 8192, 1024) 213 vs 335, (2048, 16384, 16384) 4930 vs 5118-5198,
     // (4096, 8192, 4096) a tie
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
     if (h->K >= 16384 && h->N <= 8192 && density > 0.375) return false;
