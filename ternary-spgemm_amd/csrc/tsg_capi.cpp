@@ -737,7 +737,19 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // 63.0, s = 4 at M = 48 101 vs 71)
     const bool small_w = one8 && M <= kEllSmallWMaxM &&
                          (double)M * (double)(h->nnz_pos + h->nnz_neg) <= kEllSmallWWork;
-    if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) && !starved && !small_w)
+    // ... unless the 64-row image (one launch, X read directly since round 5)
+    // is faster there even at its floor: its K sweep costs ~0.9 us per step (2
+    // passes over ceil(K / 188) chunks) + 1.4, the walk's chains ~9.9 +
+    // 0.0143 us per entry of a column (K / s); profiles/r05z_walk_vs_image2.jsonl
+    // (88 shapes with r05z_walk_vs_image_ab.jsonl: 21 within-3% misses of the
+    // round-4 rule -> 4), step us: K = 1024, s = 4, M = 48 ... 1024, N = 512 / 1024 /
+    // 4096 12.2-15.6 vs 13.6-18.8 (every M); s = 16 10.8-11.1 walk vs
+    // 11.6-12.2; K = 2048 walk 17.2 vs 19.5 (M <= 256)
+    const double nnz_col = (double)(h->nnz_pos + h->nnz_neg) / std::max(1, h->N);
+    const bool image_floor_lower =
+        0.9 * 2.0 * ((h->K + tsg::kJit64RowChunk - 1) / tsg::kJit64RowChunk) + 1.4 < 9.9 + 0.0143 * nnz_col;
+    if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) &&
+        ((!starved && !small_w) || image_floor_lower))
         return -1;
     int v = 0;
     if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
