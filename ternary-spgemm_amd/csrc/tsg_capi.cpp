@@ -741,8 +741,8 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // is faster there even at its floor: its K sweep costs ~0.9 us per step (2
     // passes over ceil(K / 188) chunks) + 1.4, the walk's chains ~9.9 +
     // 0.0143 us per entry of a column (K / s); profiles/r05z_walk_vs_image2.jsonl
-    // (88 shapes with r05z_walk_vs_image_ab.jsonl: 21 within-3% misses of the
-    // round-4 rule -> 4), step us: K = 1024, s = 4, M = 48 ... 1024, N = 512 / 1024 /
+    // (88 shapes with r05z_walk_vs_image_ab.jsonl: the round-4 rule picked the
+    // slower kernel by > 3% on 21, this one on 4), step us: K = 1024, s = 4, M = 48 ... 1024, N = 512 / 1024 /
     // 4096 12.2-15.6 vs 13.6-18.8 (every M); s = 16 10.8-11.1 walk vs
     // 11.6-12.2; K = 2048 walk 17.2 vs 19.5 (M <= 256)
     const double nnz_col = (double)(h->nnz_pos + h->nnz_neg) / std::max(1, h->N);
