@@ -100,6 +100,15 @@ def test_plan_small_m_kernel(tsg, M, K, N, kernel):
     (128, 4096, 16384, 16, "tsg_jit64_kernel"),   # 76.1 vs 80.3
     (64, 4096, 16384, 8, "tsg_jit64_kernel"),     # 63.0 vs 66.2
     (64, 2048, 8192, 2, "tsg_jit64_kernel"),      # reference case: 36.3 vs 50.2 kernel (r04q_ref_cases.jsonl)
+    # round 5: beyond M = 32 the image where its K-sweep floor is below the walk's chain floor
+    # (r05z_walk_vs_image2.jsonl, step us, image vs walk)
+    (256, 1024, 1024, 4, "tsg_jit64_kernel"),     # 12.4 vs 13.9
+    (1024, 1024, 512, 4, "tsg_jit64_kernel"),     # 15.6 vs 18.7
+    (48, 1024, 4096, 4, "tsg_jit64_kernel"),      # 12.7 vs 13.9
+    (256, 1024, 1024, 16, "tsg_tcsc_ell_kernel"),  # 12.0 vs 10.8
+    (256, 2048, 1024, 4, "tsg_tcsc_ell_kernel"),  # 19.8 vs 18.6
+    (1000, 2048, 512, 2, "tsg_jit64_kernel"),     # reference case: 30.0 vs 42.4 (r05d_ref_cases.jsonl)
+    (32, 1024, 4096, 4, "tsg_tcsc_ell_kernel"),   # configs[0]: M <= 32 stays on the walk (9.7 vs 12.5)
 ])
 def test_plan_small_w_walk(tsg, M, K, N, s, kernel):
     assert tsg.call_plan(K, N, K * N // s, M)["kernel"] == kernel
