@@ -128,7 +128,6 @@ constexpr int64_t kJitFullWgs = 230;
 constexpr int64_t kJitOneRoundWgs = 256;  // one jit workgroup per CU (144 KiB of LDS)
 constexpr double kFarXtBytes = 768.0 * 1024 * 1024;  // X^T >= 3x the 256 MiB Infinity Cache
 constexpr double kFarCodeBytes = 160.0 * 1024 * 1024;  // code image well inside it
-constexpr double kFarKeepXtBytes = 1536.0 * 1024 * 1024;  // X^T >= 6x it: the far image beats the 64-row one
 constexpr double kXDirectMinAddsPerRow = 32.0;  // 64-row image: direct X from width x density >= this
 constexpr int64_t kEllStarvedWgs = 64;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
@@ -378,23 +377,16 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     if (env_max >= 0) return M <= env_max;
     if (M <= kRows64AutoMaxM) return true;
     const JitShape s = pick_jit_shape(h, M, false);
-    // the far-X^T image (128-row only) where X^T is >= 6x the Infinity Cache:
-    // (64000, 16384, 4096) 22.1 vs 24.3 ms for the 64-row 128 x 8, while at
-    // (16000, 16384, 4096) the 64-row image wins, 4.75 vs 5.69 ms
-    // (profiles/r04p_far_ab.jsonl); round 5 with direct X on the row layout
-    // (r05z_big_images_ab.jsonl, step ms): (64000, ...) 23.4 vs 26.2, (32000,
-    // ...) -- X^T 1.95 GiB -- 11.9 vs 12.5, (16000, ...) 5.96 vs 5.23
-    if (s.far && 4.0 * (double)M * (double)h->K >= kFarKeepXtBytes) return false;
-    // dense W over long K and few columns: the 128-row image's long-stream map
-    // keeps each XCD on one column tile's code ((64000, 16384, 4096) s = 2:
-    // 39.0 vs 50.6 ms, profiles/r04m_w128_big.jsonl; round 5, step us,
-    // r05z_dense_longk2_ab.jsonl: (4096 / 8192, 16384, 4096) 2420 / 4967 vs
-    // 2507 / 5696); at K = 8192 or N = 16384 the 64-row image with direct X
-    // wins: (16000, 8192, 2048) 2393 vs 2546, (1024, 8192, 4096) 366 vs 395,
-    // (2048, 8192, 1024) 213 vs 335, (2048, 16384, 16384) 4930 vs 5118-5198,
-    // (4096, 8192, 4096) a tie
+    // Round 4 kept two regimes on the 128-row image: the far-X^T image where
+    // X^T is >= 8x the Infinity Cache ((64000, 16384, 4096) s = 4 22.1 vs 24.3
+    // ms) and dense W over long K ((64000, 16384, 4096) s = 2 39.0 vs 50.6,
+    // profiles/r04p_far_ab.jsonl, r04m_w128_big.jsonl).  Round 5's 64-row
+    // image reads X directly and takes the long-stream map there too
+    // (pick_jit_map), and wins both (step ms, each image in its own process,
+    // r05z_longk_maps_ab.jsonl, r05z_longk_maps2_ab.jsonl): (64000, 16384,
+    // 4096) s = 4 18.87-19.00 vs 23.37-23.93, s = 2 37.99 vs 39.57; (32000,
+    // ...) s = 4 9.40-9.49 vs 12.05-12.15; (8192, ...) s = 2 4.76 vs 4.94.
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
-    if (h->K >= 16384 && h->N <= 8192 && density > 0.375) return false;
     // 128 columns per wave fill whole rounds: twice the adds per staged chunk
     // and per X read of either 64-wide stream (profiles/r04l_w128_ab.jsonl,
     // r04m_w128_big.jsonl) -- for sparse W or long K, and for dense W over
@@ -569,7 +561,15 @@ void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, i
     // 13.72-13.73 ms vs 15.3-15.8 at 4 x 8, profiles/r03f_sparse_big_ab.txt);
     // s = 16 stays on 4 x 8 (8.38-8.45 vs 11.66 at 1 x 32)
     const bool long_sparse = h->K >= 8192 && density > 0.09375;
-    if (ntiles <= 4 || mtiles <= 8 || (density <= 0.1875 && !long_sparse)) {
+    // round 5: the 64-row image's 128-wide streams over K >= 16384 with dense
+    // W (s <= 4) take the long-stream map even on <= 4 column tiles -- an XCD
+    // on one tile's code, 32 M tiles in step through it (profiles/
+    // r05z_longk_maps_ab.jsonl, step ms, 1 x 32 vs 4 x 8: (64000, 16384,
+    // 4096) s = 2 / 4 37.99 / 18.87 vs 50.15 / 24.71, (16000, ...) s = 4 4.73
+    // vs 4.94, (8192, ...) s = 2 4.76 vs 4.92, s = 4 and (4096, ...) ties;
+    // s = 8 stays 4 x 8: 10.90 vs 12.99; K = 8192, N = 2048 too: 1.19 vs 1.41)
+    const bool long_dense_wide = nw == tsg::kJit64WideNW && h->K >= 16384 && density > 0.1875 && mtiles > 8;
+    if (!long_dense_wide && (ntiles <= 4 || mtiles <= 8 || (density <= 0.1875 && !long_sparse))) {
         n = 4;
         m = 8;
     } else if (h->K >= 8192) {

@@ -20,29 +20,28 @@ import pytest
     # configs[3] sparse end: 4 x 8 map (r03_map_density_ab.txt), 128 x 8 64-row (468 vs 569 us with
     # integer X, 496 vs 600 fractional, r04o), code touches thinned (444-448 vs 458-463, r04t)
     ((4096, 4096, 16384, 16), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
-    # the reference's largest case: s = 4 far-X^T image on 1 x 32 (r03e_far_ab.txt) ...
-    ((64000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
-    # ... s = 2 (code past the Infinity Cache) 128-row on 1 x 32 (r03f_sparse_big_ab.txt; the 64-row
-    # image 50.6 vs 39.0 ms, r04m_w128_big.jsonl) ...
-    ((64000, 16384, 4096, 2), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
-    # ... s = 8 / 16 on the 64-row image's 128 x 8, 4 x 8 (11.2 / 7.2 vs 14.3 / 8.7 ms, r04m), every
-    # M tile touching its code (10.8 / 7.0 vs 14.6 / 8.3 ms thinned, r05p_tmask_long_ab.jsonl)
+    # the reference's largest case, dense (s = 2 / 4): round 5 runs the 64-row image's 128 x 8 on the
+    # long-stream 1 x 32 map, X read directly (step ms vs the 128-row image -- s = 4 the far-X^T
+    # one: 18.86 vs 22.84, s = 2 38.02 vs 39.90; r05z_longk_auto.jsonl) ...
+    ((64000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
+    ((64000, 16384, 4096, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
+    # ... s = 8 / 16 on the 64-row image's 128 x 8, 4 x 8 (11.2 / 7.2 vs 14.3 / 8.7 ms, r04m; 1 x 32 at
+    # s = 8 12.99 vs 10.90, r05z_longk_maps_ab.jsonl), every M tile touching its code (10.8 / 7.0 vs
+    # 14.6 / 8.3 ms thinned, r05p_tmask_long_ab.jsonl)
     ((64000, 16384, 4096, 8), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
     ((64000, 16384, 4096, 16), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=0)),
     ((16000, 8192, 2048, 8), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 8), tmask=0)),
-    # X^T too small for the far image (r03e_long_k_ab.txt): 64-row 128 x 8 (2467 vs 2833 us, r04m) / large enough
-    ((8192, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
-    # (the far image only from X^T >= 1.5 GiB: at 1 GiB the 64-row 128 x 8 wins, 4.75 vs 5.69 ms, r04p_far_ab.jsonl;
-    # at 1.95 GiB the far image, 11.9 vs 12.5 ms step, r05z_big_images_ab.jsonl)
-    ((32000, 16384, 4096, 4), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=True, map=(1, 32), tmask=0)),
-    # dense W (s = 2) over long K: the 128-row image only for K >= 16384 with N <= 8192
-    # (r05z_dense_longk_ab.jsonl, step us: (8192, 16384, 4096) 4967 vs 5696); else the 64-row one
-    # ((16000, 8192, 2048) 2398 vs 2556, (2048, 8192, 1024) 238 vs 341, (2048, 16384, 16384) 4939 vs 5250)
-    ((8192, 16384, 4096, 2), dict(kernel="tsg_jit_kernel", width=64, waves=8, far=False, map=(1, 32), tmask=0)),
+    # dense W over K >= 16384 at any M: the same (r05z_longk_auto.jsonl, step us: (8192, 16384, 4096)
+    # s = 4 / 2 2359 / 4772 vs 2909 / 4968, (32000, ...) s = 4 9470 vs 11645, (4096, ...) s = 2 2387 vs 2435)
+    ((8192, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
+    ((32000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
+    ((8192, 16384, 4096, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
+    # dense W (s = 2) over K = 8192 (r05z_dense_longk2_ab.jsonl: (16000, 8192, 2048) 2393 vs 2546 us,
+    # (2048, 8192, 1024) 213 vs 335, (2048, 16384, 16384) 4930 vs 5118-5198)
     ((16000, 8192, 2048, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 8), tmask=3)),
     ((2048, 8192, 1024, 2), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(1, 32), tmask=3)),
     ((2048, 16384, 16384, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
-    ((16000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(4, 8), tmask=3)),
+    ((16000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
     # the 64-row image at mid M (round 4, r04d_rows64_ab.jsonl): one round of workgroups,
     # the shape of least modelled time (tsg_capi.cpp pick_jit_shape)
     ((256, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(4, 4), tmask=3)),
@@ -114,12 +113,13 @@ def test_plan_small_w_walk(tsg, M, K, N, s, kernel):
     assert tsg.call_plan(K, N, K * N // s, M)["kernel"] == kernel
 
 
-def test_plan_dense_long_k_stays_128_row(tsg):
-    """Dense W (s = 2) over long K keeps the 128-row image's long-stream map
-    ((64000, 16384, 4096) s = 2: 39.0 vs 50.6 ms, profiles/r04m_w128_big.jsonl);
-    s = 4 over long K takes the 64-row image's 128 x 8 ((8192, 16384, 4096):
-    2484 vs 2453 us int, 2476 vs 2833 frac, r04o_xdata_ab.jsonl)."""
-    assert tsg.call_plan(16384, 4096, 16384 * 4096 // 2, 4096)["kernel"] == "tsg_jit_kernel"
+def test_plan_dense_long_k_on_64_row_image(tsg):
+    """Round 5: dense W over long K runs the 64-row image on the long-stream
+    map (round 4 kept s = 2 on the 128-row image, 39.0 vs 50.6 ms on the
+    64-row one's 4 x 8 map, profiles/r04m_w128_big.jsonl; on 1 x 32 it is
+    38.02 vs 39.90, r05z_longk_auto.jsonl); the 128-row image remains for
+    calls that pin it (tcsc_hip_set_tile_rows(h, 128)) and BlockedTCSC."""
+    assert tsg.call_plan(16384, 4096, 16384 * 4096 // 2, 4096)["kernel"] == "tsg_jit64_kernel"
     assert tsg.call_plan(16384, 4096, 16384 * 4096 // 4, 8192)["kernel"] == "tsg_jit64_kernel"
 
 

@@ -36,7 +36,7 @@ def _dense_w(csp, csn, rip, rin, K, N, dev):
     (4096, 4096, 16384, 16),
     (1000, 2048, 512, 4),        # reference cases (plots/run_benchmark.py:8-33)
     (16000, 8192, 2048, 8),
-    (64000, 16384, 4096, 4),     # the reference's largest case (the far-X^T image)
+    (64000, 16384, 4096, 4),     # the reference's largest case (64-row image; the far-X^T image pinned too)
     (64000, 16384, 4096, 8),     # ... sparse, on the 1 x 32 map
     (37, 16384, 16384, 4),       # small M, K in several chunks
 ])
@@ -52,16 +52,24 @@ def test_full_y_integer_x(tsg, M, K, N, s):
     b = torch.full((N,), 2.0, device=dev)  # main.cpp:194
     Y = h.gemm_torch(X, b)
     kernel = h.call_kernel(M) + (" (far-X^T image)" if h.call_far(M) else "")
-    # the automatic far-X^T rule (tsg_capi.cpp far_xt) picks the largest case at s = 4 only
-    assert h.call_far(M) == ((M, K, N, s) == (64000, 16384, 4096, 4))
+    # round 5: no automatic call takes the far-X^T image (the 64-row image wins, tsg_capi.cpp
+    # pick_rows64); the 128-row image pinned takes it at the largest case (far_xt)
+    assert not h.call_far(M)
     W = _dense_w(csp, csn, rip, rin, K, N, dev)
     ref = torch.matmul(X, W) + b
     del W
     torch.cuda.synchronize()
     same = torch.equal(Y.view(torch.int32), ref.view(torch.int32))
     bad = int((Y.view(torch.int32) != ref.view(torch.int32)).sum()) if not same else 0
-    h.close()
     assert same, f"{bad} of {M * N} elements differ ({kernel})"
+    if (M, K, N, s) == (64000, 16384, 4096, 4):
+        h.set_tile_rows(128)
+        assert h.call_far(M) and h.call_kernel(M) == "tsg_jit_kernel"
+        del Y
+        Y = h.gemm_torch(X, b)
+        torch.cuda.synchronize()
+        assert torch.equal(Y.view(torch.int32), ref.view(torch.int32)), "far-X^T image"
+    h.close()
 
 
 def _oracle_threads() -> int:
