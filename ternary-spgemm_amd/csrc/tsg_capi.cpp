@@ -400,8 +400,14 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     // way (s = 16: 468 vs 569 int, 496 vs 600 frac).
     const bool direct_capable = x_direct_shape_ok(h->K, tsg::jit64_piece_rows()) &&
                                 x_direct_auto(h, tsg::kJit64WideNW, tsg::jit64_piece_rows());
-    if ((density <= 0.1875 || h->K >= 8192 || direct_capable) && pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW)
-        return true;
+    // round 5: whenever the 64-row image reads X directly (the row layout: K
+    // >= 188, K % 4 == 0) its call is one launch, while the 128-row image's
+    // step adds its X^T pass -- the 128-row image's whole-round shapes below
+    // lose their step too (r05z_n512_ab.jsonl, step us, M = 64000, N = 512:
+    // K = 4096 s = 4 693 vs 1093, K = 16384 2690 vs 4244, K = 1024 s = 16 170
+    // vs 261)
+    if (direct_capable) return true;
+    if ((density <= 0.1875 || h->K >= 8192) && pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW) return true;
     if (s.nw != tsg::kJitNW || s.waves != tsg::kJitWaves) return true;
     const int64_t wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
                         ((h->N + (int64_t)s.waves * s.nw - 1) / ((int64_t)s.waves * s.nw));

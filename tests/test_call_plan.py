@@ -42,6 +42,8 @@ import pytest
     ((2048, 8192, 1024, 2), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(1, 32), tmask=3)),
     ((2048, 16384, 16384, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
     ((16000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
+    # the 128-row image's whole-round shapes now lose on the step too (its X^T pass; r05z_n512_ab.jsonl)
+    ((64000, 4096, 512, 4), dict(kernel="tsg_jit64_kernel", width=64, waves=8, far=False, map=(1, 8), tmask=0)),
     # the 64-row image at mid M (round 4, r04d_rows64_ab.jsonl): one round of workgroups,
     # the shape of least modelled time (tsg_capi.cpp pick_jit_shape)
     ((256, 4096, 16384, 4), dict(kernel="tsg_jit64_kernel", width=32, waves=8, far=False, map=(4, 4), tmask=3)),
