@@ -757,6 +757,13 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) &&
         ((!starved && !small_w) || image_floor_lower))
         return -1;
+    // K in chunks (the 16-row tile, 8 columns per wave) at 8 < M <= 16: the
+    // walk needs >= 2048 waves (N >= 16384) to beat the 64-row image
+    // (r05z_walk_longk2_ab.jsonl, us, image vs walk: (16, 8192, 8192) 81.6 vs
+    // 96.4, (12, 8192, 4096) 68.7 vs 91.3, (16, 16384, 4096) 131.7 vs 181.0,
+    // (16, 8192, 2048) 66.3 vs 96.2; the walk (16, 16384, 16384) 170 vs 205,
+    // and at M <= 8 (8, 8192, 4096) 61.5 vs 68.5, r05z_walk_longk_ab.jsonl)
+    if (h->small_m < 2 && !one8 && M > 8 && h->N < 16384) return -1;
     int v = 0;
     if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
         v = kEllTile8;

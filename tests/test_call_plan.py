@@ -110,6 +110,11 @@ def test_plan_small_m_kernel(tsg, M, K, N, kernel):
     (256, 2048, 1024, 4, "tsg_tcsc_ell_kernel"),  # 19.8 vs 18.6
     (1000, 2048, 512, 2, "tsg_jit64_kernel"),     # reference case: 30.0 vs 42.4 (r05d_ref_cases.jsonl)
     (32, 1024, 4096, 4, "tsg_tcsc_ell_kernel"),   # configs[0]: M <= 32 stays on the walk (9.7 vs 12.5)
+    # K in chunks at 8 < M <= 16: the walk only with N >= 16384 (r05z_walk_longk2_ab.jsonl, image vs walk us)
+    (16, 8192, 4096, 4, "tsg_jit64_kernel"),      # 69.3 vs 96.3
+    (16, 16384, 4096, 4, "tsg_jit64_kernel"),     # 131.7 vs 181.0
+    (16, 16384, 16384, 4, "tsg_tcsc_ell_kernel"),  # 205 vs 170
+    (8, 8192, 4096, 4, "tsg_tcsc_ell_kernel"),    # 68.5 vs 61.5
 ])
 def test_plan_small_w_walk(tsg, M, K, N, s, kernel):
     assert tsg.call_plan(K, N, K * N // s, M)["kernel"] == kernel
