@@ -574,13 +574,26 @@ void pick_jit_map(const tsg_tcsc *h, int mtiles, int ntiles, int &gn, int &gm, i
     // 4096) s = 2 / 4 37.99 / 18.87 vs 50.15 / 24.71, (16000, ...) s = 4 4.73
     // vs 4.94, (8192, ...) s = 2 4.76 vs 4.92, s = 4 and (4096, ...) ties;
     // s = 8 stays 4 x 8: 10.90 vs 12.99; K = 8192, N = 2048 too: 1.19 vs 1.41)
-    const bool long_dense_wide = nw == tsg::kJit64WideNW && h->K >= 16384 && density > 0.1875 && mtiles > 8;
+    // (and K = 8192 with >= 4 column tiles: (64000, 8192, 4096) s = 4 10.91 vs
+    // 12.86, (32000, 8192, 4096) s = 2 9.08 vs 12.20; with 2 column tiles 4 x 8
+    // (gn = 2) stays: (64000, 8192, 2048) a tie, (16000, 8192, 2048) 1.19 vs
+    // 1.41; r05z_k8192_maps_ab.jsonl)
+    // The 64-row image takes the long-stream map only with >= 64-column
+    // streams and >= 32 M tiles (a full group): narrower streams and half
+    // groups run faster on 4 x 8 (r05z_midm_longk_maps_ab.jsonl, us, 4 x 8
+    // vs 1 x 32 / 1 x 16: (1024, 16384, 4096) 32 x 8 374 vs 471, (2048, 8192,
+    // 1024) s = 2 16 x 8 165 vs 210, (1024, 8192, 16384) 128 x 8 600 vs 630;
+    // the long map (2048, 16384, 4096) 64 x 8 622 vs 709, (2048, 16384,
+    // 16384) s = 2 4929 vs 6014)
+    const bool long_ok = nw == 0 || (nw >= 64 && mtiles >= 32);
+    const bool long_dense_wide = nw == tsg::kJit64WideNW && h->K >= 8192 && density > 0.1875 && mtiles >= 32 &&
+                                 (h->K >= 16384 || ntiles >= 4);
     if (!long_dense_wide && (ntiles <= 4 || mtiles <= 8 || (density <= 0.1875 && !long_sparse))) {
         n = 4;
         m = 8;
     } else if (h->K >= 8192) {
-        n = 1;
-        m = 32;
+        n = long_dense_wide || long_ok ? 1 : 4;
+        m = long_dense_wide || long_ok ? 32 : 8;
     }
     gn = std::min(env_gn > 0 ? env_gn : n, std::max(ntiles, 1));  // a group never exceeds the grid
     gm = std::min(env_gm > 0 ? env_gm : m, std::max(mtiles, 1));

@@ -39,7 +39,8 @@ import pytest
     # dense W (s = 2) over K = 8192 (r05z_dense_longk2_ab.jsonl: (16000, 8192, 2048) 2393 vs 2546 us,
     # (2048, 8192, 1024) 213 vs 335, (2048, 16384, 16384) 4930 vs 5118-5198)
     ((16000, 8192, 2048, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(2, 8), tmask=3)),
-    ((2048, 8192, 1024, 2), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(1, 32), tmask=3)),
+    # (its 16-column streams on 4 x 8: 165 vs 210 us on 1 x 32, r05z_midm_longk_maps_ab.jsonl)
+    ((2048, 8192, 1024, 2), dict(kernel="tsg_jit64_kernel", width=16, waves=8, far=False, map=(4, 8), tmask=3)),
     ((2048, 16384, 16384, 2), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
     ((16000, 16384, 4096, 4), dict(kernel="tsg_jit64_kernel", width=128, waves=8, far=False, map=(1, 32), tmask=3)),
     # the 128-row image's whole-round shapes now lose on the step too (its X^T pass; r05z_n512_ab.jsonl)
