@@ -103,7 +103,9 @@ struct tsg_tcsc {
     int ring_head = 0, ring_count = 0;    // pending pairs: [head - count, head)
     double total_ms = 0.0;
     int64_t launches = 0;
-    std::mutex mu;
+    // run_dev, reserve and the setters write the plan state (bad_variants,
+    // JitVariant, pins) under it; the const per-call queries read under it too
+    mutable std::mutex mu;
 };
 
 namespace {
@@ -128,8 +130,13 @@ constexpr int64_t kJitFullWgs = 230;
 constexpr int64_t kJitOneRoundWgs = 256;  // one jit workgroup per CU (144 KiB of LDS)
 constexpr double kFarXtBytes = 768.0 * 1024 * 1024;  // X^T >= 3x the 256 MiB Infinity Cache
 constexpr double kFarCodeBytes = 160.0 * 1024 * 1024;  // code image well inside it
+constexpr double kFarKeepXtBytes = 1536.0 * 1024 * 1024;  // X^T >= 6x it: the far image beats the staged 64-row one
 constexpr double kXDirectMinAddsPerRow = 32.0;  // 64-row image: direct X from width x density >= this
 constexpr int64_t kEllStarvedWgs = 64;
+// the 64-row image's step when it cannot read X directly: its X^T staging
+// launch (tsg_transpose_rows_kernel) ahead of the image, at the walk's M
+// (X <= 20 MB) -- r06_staged_floor_ab.jsonl
+constexpr double kStagedXtUs = 5.0;
 static_assert(tsg::kEllTileM[kEllTile8] == 8, "kEllTile8 is the 8-row tile");
 
 struct DeviceGuard {
@@ -331,12 +338,14 @@ bool x_direct_shape_ok(int K, int piece_rows)
     return piece_rows == 0 ? K >= tsg::kJit64RowChunk && K % 4 == 0 : K > 0 && K % (256 / piece_rows) == 0;
 }
 
+// the dispatcher's per-lane X offsets are 32-bit
+bool x_direct_offsets_ok(int M, int K) { return (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32); }
+
 bool x_direct(const tsg_tcsc *h, const float *dX, int M, int K, const tsg_tcsc::JitVariant &jv)
 {
     const char *e = tsg::knob_value("TSG_JIT_XDIRECT");
     const bool on = e ? e[0] == '1' : x_direct_auto(h, jv.nw, jv.piece_rows);
-    return on && x_direct_shape_ok(K, jv.piece_rows) && ((uintptr_t)dX & 15) == 0 &&
-           (int64_t)M * K * 4 + 4096 < ((int64_t)1 << 32);
+    return on && x_direct_shape_ok(K, jv.piece_rows) && ((uintptr_t)dX & 15) == 0 && x_direct_offsets_ok(M, K);
 }
 
 JitShape pick_jit_shape(const tsg_tcsc *h, int M, bool r64 = false);
@@ -398,8 +407,11 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     // configs[2] 1239.4 vs 1248.8 us per step with integer X
     // (r04z_direct_big_ab.jsonl); the sparse end is the 64-row image's either
     // way (s = 16: 468 vs 569 int, 496 vs 600 frac).
+    // x_direct's own limits that M and K decide (the 32-bit per-lane offsets:
+    // X below 4 GiB); X's alignment is checked per call
     const bool direct_capable = x_direct_shape_ok(h->K, tsg::jit64_piece_rows()) &&
-                                x_direct_auto(h, tsg::kJit64WideNW, tsg::jit64_piece_rows());
+                                x_direct_auto(h, tsg::kJit64WideNW, tsg::jit64_piece_rows()) &&
+                                x_direct_offsets_ok(M, h->K);
     // round 5: whenever the 64-row image reads X directly (the row layout: K
     // >= 188, K % 4 == 0) its call is one launch, while the 128-row image's
     // step adds its X^T pass -- the 128-row image's whole-round shapes below
@@ -407,6 +419,16 @@ bool pick_rows64(const tsg_tcsc *h, int M)
     // K = 4096 s = 4 693 vs 1093, K = 16384 2690 vs 4244, K = 1024 s = 16 170
     // vs 261)
     if (direct_capable) return true;
+    // X past the 32-bit offsets: both images stage X, as in round
+    // 4, whose two rules for that regime stand -- the far-X^T image (128-row
+    // only) where X^T is >= 6x the Infinity Cache ((64000, 16384, 4096) 22.1
+    // vs 24.3 ms for the 64-row 128 x 8, profiles/r04p_far_ab.jsonl), and the
+    // 128-row long-stream map for dense W over long K with few columns
+    // ((64000, 16384, 4096) s = 2 39.0 vs 50.6 ms, r04m_w128_big.jsonl)
+    if (x_direct_shape_ok(h->K, tsg::jit64_piece_rows()) && !x_direct_offsets_ok(M, h->K)) {
+        if (s.far && 4.0 * (double)M * (double)h->K >= kFarKeepXtBytes) return false;
+        if (h->K >= 16384 && h->N <= 8192 && density > 0.375) return false;
+    }
     if ((density <= 0.1875 || h->K >= 8192) && pick_jit_shape(h, M, true).nw == tsg::kJit64WideNW) return true;
     if (s.nw != tsg::kJitNW || s.waves != tsg::kJitWaves) return true;
     const int64_t wgs = (int64_t)((M + tsg::kJitTileM - 1) / tsg::kJitTileM) *
@@ -764,9 +786,14 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // slower kernel by > 3% on 21, this one on 4), step us: K = 1024, s = 4, M = 48 ... 1024, N = 512 / 1024 /
     // 4096 12.2-15.6 vs 13.6-18.8 (every M); s = 16 10.8-11.1 walk vs
     // 11.6-12.2; K = 2048 walk 17.2 vs 19.5 (M <= 256)
+    // (this floor was measured with X read directly, one launch: with K % 4 !=
+    // 0 or X past the 32-bit offsets the image's step also runs its X^T
+    // staging kernel, priced here at kStagedXtUs -- ADVICE r05)
+    const bool image_one_launch = x_direct_shape_ok(h->K, tsg::jit64_piece_rows()) && x_direct_offsets_ok(M, h->K);
     const double nnz_col = (double)(h->nnz_pos + h->nnz_neg) / std::max(1, h->N);
-    const bool image_floor_lower =
-        0.9 * 2.0 * ((h->K + tsg::kJit64RowChunk - 1) / tsg::kJit64RowChunk) + 1.4 < 9.9 + 0.0143 * nnz_col;
+    const bool image_floor_lower = 0.9 * 2.0 * ((h->K + tsg::kJit64RowChunk - 1) / tsg::kJit64RowChunk) + 1.4 +
+                                       (image_one_launch ? 0.0 : kStagedXtUs) <
+                                   9.9 + 0.0143 * nnz_col;
     if (h->small_m < 2 && M > (one8 ? auto_max : std::min(auto_max, kEllAutoMaxMChunked)) &&
         ((!starved && !small_w) || image_floor_lower))
         return -1;
@@ -776,6 +803,8 @@ int pick_ell_variant(const tsg_tcsc *h, int M)
     // 96.4, (12, 8192, 4096) 68.7 vs 91.3, (16, 16384, 4096) 131.7 vs 181.0,
     // (16, 8192, 2048) 66.3 vs 96.2; the walk (16, 16384, 16384) 170 vs 205,
     // and at M <= 8 (8, 8192, 4096) 61.5 vs 68.5, r05z_walk_longk_ab.jsonl)
+    // (measured with direct X; the image's margin, 15-50 us, exceeds its X^T
+    // pass at these M -- 16 x 8194 floats -- so the rule holds staged too)
     if (h->small_m < 2 && !one8 && M > 8 && h->N < 16384) return -1;
     int v = 0;
     if (one8 && M > tsg::kEllTileM[kEllTile8] && M <= kEllMidM) {
@@ -1521,12 +1550,14 @@ extern "C" int tcsc_hip_set_jit_width(tsg_tcsc *h, int width)
 extern "C" int tcsc_hip_jit_width(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
     return call_shape(h, M).nw;
 }
 
 extern "C" int tcsc_hip_jit_waves(const tsg_tcsc *h, int M)
 {
     if (!h || h->kind != tsg_tcsc::kJit) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
     return call_shape(h, M).waves;
 }
 
@@ -1544,6 +1575,7 @@ extern "C" int tcsc_hip_set_tile_rows(tsg_tcsc *h, int rows)
 extern "C" int tcsc_hip_call_launches(const tsg_tcsc *h, const float *dX, int M)
 {
     if (!h || M <= 0) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
     if (pick_ell_variant(h, M) >= 0) return 1;
     if (h->kind != tsg_tcsc::kJit) return 2;
     const JitShape sh = call_shape(h, M);
@@ -1558,7 +1590,9 @@ extern "C" int tcsc_hip_call_launches(const tsg_tcsc *h, const float *dX, int M)
 
 extern "C" int tcsc_hip_call_tile_rows(const tsg_tcsc *h, int M)
 {
-    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
+    if (!h) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
     return call_shape(h, M).r64 ? tsg::kJit64TileM : tsg::kJitTileM;
 }
 
@@ -1609,7 +1643,9 @@ extern "C" int tcsc_hip_set_far(tsg_tcsc *h, int mode)
 
 extern "C" int tcsc_hip_call_far(const tsg_tcsc *h, int M)
 {
-    if (!h || h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
+    if (!h) return 0;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->kind != tsg_tcsc::kJit || M <= 0 || pick_ell_variant(h, M) >= 0) return 0;
     const JitShape sh = call_shape(h, M);
     return !sh.r64 && sh.far ? 1 : 0;
 }
@@ -1664,6 +1700,7 @@ extern "C" int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int 
 extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)
 {
     if (!h) return "";
+    std::lock_guard<std::mutex> lk(h->mu);
     const int ev = pick_ell_variant(h, M);
     if (ev >= 0) return use_ell_pc(h, ev) ? "tsg_tcsc_ell_pc_kernel" : "tsg_tcsc_ell_kernel";
     if (h->kind == tsg_tcsc::kJit && call_shape(h, M).r64) return "tsg_jit64_kernel";

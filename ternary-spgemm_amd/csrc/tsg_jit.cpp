@@ -429,6 +429,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         }
     };
     int base_chunk = -1;  // chunk whose base s[84:85] holds
+    bool base_adj = false;  // that base already carries the last chunk's s87 adjustment
     // stage step q's chunk into LDS buffer q % kJitRing: the chunk base, then
     // pieces 0..kPieces-1 (dma_piece); M0 = s83 (this wave's first piece, set
     // by the dispatcher) + buffer + piece offset (m0k: the first of 4 pieces'
@@ -438,15 +439,19 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         if (j == 0 || base_chunk < 0 || j < base_chunk) {
             E.base_reset();
             for (int i = 0; i < j; i++) E.base_next();
+            base_adj = false;
         } else {
             for (int i = base_chunk; i < j; i++) E.base_next();
         }
         base_chunk = j;
-        if (rowlay && j == nch - 1 && jit64_row_kbase(K, nch, j) != j * CH) {
+        if (rowlay && j == nch - 1 && jit64_row_kbase(K, nch, j) != j * CH && !base_adj) {
             // direct X: the last chunk starts s87 = 4 (188 nch - K) bytes below its
-            // slot (the staged copy holds it in its slot: s87 = 0); a later
-            // chunk never follows it without a base reset
+            // slot (the staged copy holds it in its slot: s87 = 0); applied once
+            // per arrival on the last chunk (a step that stages it again keeps
+            // the adjusted base), and a later chunk never follows it without a
+            // base reset
             E.base_last_adj();
+            base_adj = true;
         }
         E.nop(4);  // SALU-written SGPR base -> VMEM
     };

@@ -158,3 +158,35 @@ def test_ell_maxm_knob_leaves_small_w_rule():
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr
         assert r.stdout.split() == ["tsg_tcsc_ell_kernel", "tsg_jit64_kernel"], (env_val, r.stdout)
+
+
+def test_plan_x_past_32bit_offsets_keeps_round4_rules(tsg):
+    """the 64-row image reads X directly only while M x K x 4 + 4 KiB
+    fits the dispatcher's 32-bit per-lane offsets.  Past that (M >= 65536 at
+    K = 16384) both images stage X, and round 4's rules for that regime hold:
+    the far-X^T 128-row image for X^T >= 6x the Infinity Cache ((64000, 16384,
+    4096) s = 4 22.1 vs 24.3 ms against the staged 64-row 128 x 8,
+    profiles/r04p_far_ab.jsonl) and the 128-row image for dense W over long K
+    (s = 2: 39.0 vs 50.6 ms, r04m_w128_big.jsonl).  Just inside the limit the
+    round-5 direct-X plan stands."""
+    K, N = 16384, 4096
+    inside = tsg.call_plan(K, N, K * N // 4, 65535 - 64)
+    assert inside["kernel"] == "tsg_jit64_kernel" and inside["map"] == (1, 32), inside
+    far = tsg.call_plan(K, N, K * N // 4, 65536)
+    assert far["kernel"] == "tsg_jit_kernel" and far["far"] is True, far
+    dense = tsg.call_plan(K, N, K * N // 2, 65536)
+    assert dense["kernel"] == "tsg_jit_kernel", dense
+
+
+@pytest.mark.parametrize("M,K,N,kernel", [
+    # ADVICE r05: the image-floor rule prices the X^T staging launch when the image cannot read X
+    # directly (K % 4 != 0): (256, 1024, 1024) s = 4 takes the image (12.4 vs 13.9 us direct), the
+    # same at K = 1022 the walk (image floor 12.2 + 5 us staged vs the walk's 13.6)
+    (256, 1024, 1024, "tsg_jit64_kernel"),
+    (256, 1022, 1024, "tsg_tcsc_ell_kernel"),
+    # the chunked-K rule at 8 < M <= 16 keeps the image staged too (its margin is 15-50 us)
+    (16, 8194, 4096, "tsg_jit64_kernel"),
+    (16, 8192, 4096, "tsg_jit64_kernel"),
+])
+def test_plan_staged_image_rules(tsg, M, K, N, kernel):
+    assert tsg.call_plan(K, N, K * N // 4, M)["kernel"] == kernel
