@@ -269,7 +269,7 @@ def headline(world: int, steps: int, flops_all: int, compute_elapsed_max: float,
 
 
 def build_line(a, *, world, mode, backend, M, K, Nr, Ntot, s, nnz, nnz_all, kname, compute_elapsed_max,
-               kern_ms_max, gather=None, traffic=None, cpu=None, e2e=None, stream_ms=None, setup_s=0.0,
+               kern_ms_max, gather=None, traffic=None, traffic_fs2=None, plan_asserted=False, cpu=None, e2e=None, stream_ms=None, setup_s=0.0,
                clock_warmup=(0.0, 0), kernel_timing=None) -> dict:
     """The JSON line rank 0 prints (bench.py contract), from the measured
     quantities (max over ranks).  Pure: tests/test_bench_launch.py checks it
@@ -324,7 +324,11 @@ def build_line(a, *, world, mode, backend, M, K, Nr, Ntot, s, nnz, nnz_all, knam
                      "kernel": kname, "kernel_ms": round(kern_ms_max, 4), "kernel_timing": kernel_timing,
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "kernel_gflops": round(adds / (kern_ms_max * 1e-3) / 1e9, 2),
-                     "traffic_source": (os.path.relpath(PROFILE_PMC, REPO) if traffic is not None else None),
+                     "traffic_source": (os.path.relpath(PROFILE_PMC, REPO) + " (read bytes by request size "
+                                        "TCC_EA0_RDREQ_{32,64,128}B + WRITE_SIZE"
+                                        + ("; plan asserted)" if plan_asserted else ")")
+                                        if traffic is not None else None),
+                     "traffic_fetch_size_x2": traffic_fs2,
                      "binding": {"resource": "valu fp32 adds (DESIGN.md 4)", "adds_per_launch": adds,
                                  "achieved_Tadds": round(adds / (kern_ms_max * 1e-3) / 1e12, 2),
                                  "peak_Tadds": round(VALU_PEAK_TADDS, 2), "frac": binding_frac}},
@@ -576,20 +580,29 @@ def main():
         cpu = cpu_baseline(X, csp, csn, rip, rin, K, Nr, s, Y, a.cpu_rows)
 
     if rank == 0:
-        traffic = None
+        traffic = traffic_fs2 = None
+        plan_asserted = False
         try:
             # HBM bytes per launch of THIS kernel on THIS workload, from the
             # committed rocprofv3 PMC passes (scripts/pmc_summary.py: FETCH_SIZE
             # and WRITE_SIZE with the gfx950 corrections of MI355X_MICROARCH.md)
             pm = json.load(open(PROFILE_PMC))
-            if pm.get("workload") == f"{M}x{K}x{Nr}s{s}" and pm.get("kernel") == kname:
-                traffic = pm.get("kernels", {}).get(kname, {}).get("hbm_bytes")
+            plan = {k: list(v) if isinstance(v, tuple) else v for k, v in T.call_plan(K, Nr, nnz, M).items()}
+            if (pm.get("workload") == f"{M}x{K}x{Nr}s{s}" and pm.get("kernel") == kname
+                    and pm.get("plan", plan) == plan):  # (summaries before round 6 carry no plan)
+                kp = pm.get("kernels", {}).get(kname, {})
+                # read bytes by memory-side request size + WRITE_SIZE (VERDICT
+                # r05: FETCH_SIZE x 2 overstated this kernel's reads by ~7%)
+                traffic = kp.get("hbm_bytes_by_request_size", kp.get("hbm_bytes"))
+                traffic_fs2 = kp.get("hbm_bytes")
+                plan_asserted = "plan" in pm
         except Exception:
             pass
         out = build_line(a, world=world, mode=mode, backend=backend, M=M, K=K, Nr=Nr, Ntot=Ntot, s=s, nnz=nnz,
                          nnz_all=nnz_all, kname=kname, compute_elapsed_max=elapsed_max, kern_ms_max=kern_ms_max,
-                         gather=gather, traffic=traffic, cpu=cpu, e2e=e2e, stream_ms=stream_ms,
-                         setup_s=setup_s, clock_warmup=(clock_warmup_s, n_clock),
+                         gather=gather, traffic=traffic, traffic_fs2=traffic_fs2,
+                         plan_asserted=plan_asserted, cpu=cpu, e2e=e2e,
+                         stream_ms=stream_ms, setup_s=setup_s, clock_warmup=(clock_warmup_s, n_clock),
                          kernel_timing={"launches_per_step": step_launches,
                                         "kernel_ms_source": ("HIP events on the kernel's stream over the timed "
                                                              "region / K (one launch per step, back to back)"

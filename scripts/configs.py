@@ -77,7 +77,9 @@ def main():
                           "valu_frac": round(adds / (ms * 1e-3) / 78.64e12, 4),
                           "jit_width": jw, "jit_waves": h.jit_waves(M), "width_pinned": bool(width),
                           "far_image": h.call_far(M),
-                          "workgroups": -(-M // 128) * -(-N // (h.jit_waves(M) * max(jw, 1))),
+                          # the call's own M tile (64 rows on the 64-row image, 128 on the 128-row one)
+                          "workgroups": (-(-M // h.call_tile_rows(M)) * -(-N // (h.jit_waves(M) * max(jw, 1)))
+                                         if h.call_tile_rows(M) else None),
                           "register_s": round(reg_s, 2),
                           "bit_identical_rows": ok}), flush=True)
         h.close()

@@ -81,6 +81,16 @@ for name, g in tot:
 tot = {(name if g == biggest[name] else f"{name} [grid {g}]"): v for (name, g), v in tot.items()}
 disp = {(name if g == biggest[name] else f"{name} [grid {g}]"): v for (name, g), v in disp.items()}
 out = {"workload": f"{M}x{K}x{N}s{s}", "kernel": None, "kernels": {}, "per_launch_hbm_bytes": {}}
+# the plan the library picks for this workload (host only; exactly K N / s
+# nonzeros, as the bench's W): bench.py uses these counters only while its
+# own call runs the same plan
+try:
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ternary-spgemm_amd"))
+    import tspgemm
+    out["plan"] = {k: list(v) if isinstance(v, tuple) else v for k, v in tspgemm.call_plan(K, N, K * N // s, M).items()}
+except Exception as e:  # noqa: BLE001 -- the summary is still useful without it
+    out["plan"] = None
+    print("no plan:", e, file=sys.stderr)
 for kn, v in tot.items():
     per = {c: sum(x / max(len(disp[kn][c][f]), 1) for f, x in passes.items()) / len(passes)
            for c, passes in v.items()}
@@ -100,6 +110,10 @@ for kn, v in tot.items():
         o["hbm_read_bytes_by_request_size"] = 32 * ea[0] + 64 * ea[1] + 128 * ea[2]
         if "FETCH_SIZE" in per and per["FETCH_SIZE"]:
             o["read_bytes_over_fetch_size_bytes"] = o["hbm_read_bytes_by_request_size"] / (per["FETCH_SIZE"] * 1024)
+        if "WRITE_SIZE" in per:
+            # round 6: the traffic bench.py reports -- read bytes
+            # by request size + WRITE_SIZE; FETCH_SIZE x 2 stays beside it
+            o["hbm_bytes_by_request_size"] = o["hbm_read_bytes_by_request_size"] + per["WRITE_SIZE"] * 1024
     if "SQC_ICACHE_BUSY_CYCLES" in per and "GRBM_GUI_ACTIVE" in per:
         # summed over the instruction caches (one SQC per CU pair: 128 on the chip);
         # GRBM_GUI_ACTIVE over the 8 XCDs

@@ -653,9 +653,12 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
         return fail(TSG_ERR_RANGE, "jit image of " + std::to_string((uint64_t)img.code.size() * 4) +
                                        " B exceeds the 32-bit stream offsets; shard W's columns");
 #ifdef TSG_DIAG
-    if (nw == tsg::kJitNW && waves == tsg::kJitWaves && !r64)
+    if (!h->B)
         if (const char *d = tsg::knob_value("TSG_JIT_DIAG")) {  // diagnostic code sharing (results WRONG)
-            const size_t S = tsg::kJitStreams;
+            const size_t S = (size_t)waves;  // streams per column tile
+            if (std::strstr(d, "simdpair"))  // waves w and w + S/2 (one SIMD) share w's stream
+                for (size_t k = 0; k < img.wcode.size(); k++)
+                    if (k % S >= S / 2) img.wcode[k] = img.wcode[k - S / 2];
             if (std::strstr(d, "samecode"))  // every column tile runs tile 0's streams
                 for (size_t k = S; k < img.wcode.size(); k++) img.wcode[k] = img.wcode[k % S];
             if (std::strstr(d, "samewave"))  // every wave of a tile runs its wave 0's stream

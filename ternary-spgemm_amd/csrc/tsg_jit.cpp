@@ -336,6 +336,14 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     const bool stagger = sv && sv[0] == '1' && waves == 8 && !B && lag == 1;
     const char *pv = knob_value("TSG_JIT_PRIO");
     const bool prio = pv && pv[0] == '1' && waves == 8;
+    // TSG_JIT_MIX="reads,dma" (A/B, 0|1 each): a read group's read-ahead
+    // (ds_read) and its share of the DMA pieces go out spread evenly among
+    // the group's adds instead of in a burst before them (not with the
+    // stagger).  Slot safety is unchanged: the read-ahead of group [i0, i0 +
+    // G) refills the previous group's slots only (RA + G <= S).
+    int mix_reads = 0, mix_dma = 0;
+    if (const char *mv = knob_value("TSG_JIT_MIX")) std::sscanf(mv, "%d,%d", &mix_reads, &mix_dma);
+    if (stagger) mix_reads = mix_dma = 0;
     // X slots: all of v[8 : 104) for BaseTCSC; BlockedTCSC keeps y of half the
     // columns (nw registers) at the top of that range
     const int S = B ? (kJitXRegs - nw) / kJitSlotRegs : kJitSlots;
@@ -646,9 +654,11 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     issue_reads(g1, q);  // (only if the schedule left the group unread)
                     wait_reads(g1);
                     // (early waves before their barrier: this step's chunk only)
-                    issue_reads(g1 + RA, lag == 2 || !released ? q : q + 1);
-                    if (dma && grp >= mid && grp - mid < span && pieces_out < kPieces)  // this group's share
-                        pieces_upto(std::min(kPieces, ((grp - mid + 1) * kPieces + span - 1) / span));
+                    const int qra = lag == 2 || !released ? q : q + 1;
+                    // this group's share of the DMA pieces
+                    const int pieces_to = dma && grp >= mid && grp - mid < span && pieces_out < kPieces
+                                              ? std::min(kPieces, ((grp - mid + 1) * kPieces + span - 1) / span)
+                                              : pieces_out;
                     // per column its entries of the group (ascending k); columns in pairs, interleaved
                     std::vector<std::vector<uint32_t>> xs(nw);
                     for (int i = i0; i < i1; i++) {
@@ -656,11 +666,46 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         for (int half = 0; half < U; half++)
                             for (uint8_t col : rd.cols[half]) xs[col].push_back(xreg(first[q] + i, rd, half));
                     }
+                    std::vector<std::pair<int, uint32_t>> adds;
                     for (int col = sp.c0; col < sp.c1; col += 2)
                         for (size_t k = 0; k < std::max(xs[col].size(), xs[col + 1].size()); k++) {
-                            if (k < xs[col].size()) add(col, xs[col][k]);
-                            if (k < xs[col + 1].size()) add(col + 1, xs[col + 1][k]);
+                            if (k < xs[col].size()) adds.emplace_back(col, xs[col][k]);
+                            if (k < xs[col + 1].size()) adds.emplace_back(col + 1, xs[col + 1][k]);
                         }
+                    // the group's read-ahead and DMA pieces: before its adds
+                    // (default), or spread evenly among them (TSG_JIT_MIX)
+                    int64_t reads_to = issued;
+                    {
+                        const int qm = std::min(qra, steps - 1);
+                        reads_to = std::max(issued, std::min<int64_t>(g1 + RA, first[qm + 1]));
+                    }
+                    if (!mix_reads) issue_reads(g1 + RA, qra);
+                    if (!mix_dma) pieces_upto(pieces_to);
+                    const int nr = mix_reads ? (int)(reads_to - issued) : 0;
+                    const int np = mix_dma ? pieces_to - pieces_out : 0;
+                    const int items = nr + np, na = (int)adds.size();
+                    int done = 0, ri = 0, pi = 0;
+                    auto emit_item = [&] {
+                        // alternate reads and pieces, reads first, in proportion
+                        const bool rd = pi >= np || (ri < nr && (int64_t)ri * np <= (int64_t)pi * nr);
+                        if (rd) {
+                            issue_reads(issued + 1, qra);
+                            ri++;
+                        } else {
+                            pieces_upto(pieces_out + 1);
+                            pi++;
+                        }
+                        done++;
+                    };
+                    for (int a = 0; a < na; a++) {
+                        add(adds[(size_t)a].first, adds[(size_t)a].second);
+                        // item j goes after add (j + 1) * na / (items + 1), on an
+                        // 8-byte boundary (an odd position waits one more add)
+                        while (done < items && (int64_t)(a + 1) * (items + 1) >= (int64_t)(done + 1) * na &&
+                               (!(E.c.size() & 1) || a + 1 == na))
+                            emit_item();
+                    }
+                    while (done < items) emit_item();
                 }
                 if (sp.flush)  // comp.h:642: Y += y (a block without entries adds +0: a no-op, Y is never -0)
                     for (int col = sp.c0; col < sp.c1; col++)

@@ -97,7 +97,7 @@ bool diag_ok(const char *v)
 {
     for (const auto &s : fields(v))
         if (!one_of(s.c_str(), {"nobar", "nodma", "notouch", "nolgkm", "noreads", "novm", "samecode", "samewave",
-                                "pairwave"}))
+                                "pairwave", "simdpair"}))
             return false;
     return true;
 }
@@ -128,6 +128,8 @@ const Knob kKnobs[] = {
     {"TSG_JIT_CP", "dma,touch (hex, bits of 0x2030000)", cp_ok},
     {"TSG_JIT_TOUCH", "first,count (8-KiB units, count <= 4)", touch_ok},
     {"TSG_JIT_READS", "G,RA (G >= 1, G + RA <= 24)", reads_ok},
+    {"TSG_JIT_MIX", "reads,dma (0|1 each)",
+     [](const char *v) { return one_of(v, {"0,0", "0,1", "1,0", "1,1"}); }},
     {"TSG_JIT_DIR", "a directory", [](const char *v) { return *v != '\0'; }},
     {"TSG_ELL_PC", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_ELL_MAXM", "0..1024", [](const char *v) { return int_in(v, 0, 1024); }},
@@ -140,7 +142,7 @@ const Knob kKnobs[] = {
     {"TSG_ELL_WPG", "4 | 8 | 16", [](const char *v) { return one_of(v, {"4", "8", "16"}); }},
     {"TSG_ELL_SCHED", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
 #ifdef TSG_DIAG
-    {"TSG_JIT_DIAG", "nobar,nodma,notouch,nolgkm,noreads,novm,samecode,samewave,pairwave", diag_ok},
+    {"TSG_JIT_DIAG", "nobar,nodma,notouch,nolgkm,noreads,novm,samecode,samewave,pairwave,simdpair", diag_ok},
 #endif
 };
 

@@ -713,3 +713,26 @@ def test_jit_code_stagger_and_priority(tsg, oracle_mod, monkeypatch, knobs, M, K
         monkeypatch.setenv(k, v)
     for frac in (False, True):
         _check(tsg, oracle_mod, M, K, N, s, 11 + K, frac, width=width, waves=8, rows64=rows64)
+
+
+@pytest.mark.parametrize("mix", ["1,0", "0,1", "1,1"])
+@pytest.mark.parametrize("M,K,N,s,width,waves,rows64", [(130, 400, 520, 4, 64, 8, False), (70, 500, 1100, 4, 128, 8, True),
+                                                        (64, 1000, 300, 16, 16, 8, True), (5, 97, 40, 2, 8, 4, True),
+                                                        (200, 188, 600, 8, 32, 8, True), (64, 900, 700, 4, 16, 4, True),
+                                                        (1, 1, 1, 1, 64, 8, True)])
+def test_jit_code_mixed_issue(tsg, oracle_mod, monkeypatch, mix, M, K, N, s, width, waves, rows64):
+    """TSG_JIT_MIX (round 6, A/B): a read group's read-ahead and its share of
+    the DMA pieces spread among the group's adds instead of a burst before
+    them.  The emulated workgroup checks every X slot reload against its wait,
+    every LDS read against landed pieces and every DMA against reads since its
+    issue -- and the result equals the oracle bit for bit."""
+    monkeypatch.setenv("TSG_JIT_MIX", mix)
+    for frac in (False, True):
+        _check(tsg, oracle_mod, M, K, N, s, 13 + K, frac, width=width, waves=waves, rows64=rows64)
+
+
+def test_jit_code_mixed_issue_blocked(tsg, oracle_mod, monkeypatch):
+    """TSG_JIT_MIX with BlockedTCSC (per-block sums in the generated code)."""
+    monkeypatch.setenv("TSG_JIT_MIX", "1,1")
+    for frac in (False, True):
+        _check_blocked(tsg, oracle_mod, 130, 512, 300, 4, 128, 7, frac)
