@@ -400,6 +400,18 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // the prefetch must stay inside the tail padding past the last stream
     if ((touch_first + touch_count) * 8192u > (uint32_t)kTailPad * 4u) touch_first = (uint32_t)kTailPad * 4u / 8192u - touch_count;
     const uint32_t ntouch = d_notouch || far ? 0u : touch_count;
+    // TSG_JIT_TROLL=n (A/B; 0 = off): rolling code touches -- instead of
+    // `count` touches of 8 KiB at a fixed distance every step, each step
+    // (after its last DMA piece, as before) touches the next untouched 8-KiB
+    // windows until the stream is covered (touch_first + n) x 8 KiB ahead of
+    // the current position: a step whose code is longer than 8 KiB (128-wide
+    // streams: ~12.6 KiB at s = 4) gets all of it prefetched, a short one
+    // (16-wide: ~2 KiB) touches every few steps.  The step's closing vmcnt
+    // lets exactly the step's touches run on.  Not with the stagger or lag 2.
+    uint32_t troll = 0;
+    if (const char *tr = knob_value("TSG_JIT_TROLL")) troll = (uint32_t)std::atoi(tr);
+    const bool rolling = troll > 0 && ntouch > 0 && !stagger && lag == 1;
+    if (rolling && (touch_first + troll) * 8192u > (uint32_t)kTailPad * 4u) troll = (uint32_t)kTailPad * 4u / 8192u - touch_first;
 
     int n0 = 0;  // first column of the current stream
     std::vector<int32_t> cur((size_t)nw * 2), end((size_t)nw * 2);
@@ -464,6 +476,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         E.nop(4);  // SALU-written SGPR base -> VMEM
     };
     int vm_step = 0;  // VMEM operations (DMA pieces, code touches) issued in the current step
+    uint32_t touch_step = 0;  // rolling code touches issued in the current step
+    uint32_t touched_to = 0;  // rolling: region offset up to which the stream's code is touched
     int cur_wave = 0;  // the wave whose stream is being generated
     auto dma_piece = [&](int q, int i) {
         // 64-row image: piece pr holds quads PQ * (pr / (64 / PR)) .. + PQ - 1
@@ -521,6 +535,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             n0 = t * tile_cols + w * nw;
             std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
+            touched_to = 0;
             const bool early = stagger && w < waves / 2;  // runs half a step ahead of waves w + 4
             if (prio && w >= waves / 2) E.setprio(1);
             E.save_m0();
@@ -605,6 +620,21 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 // every DMA piece but lets the touches (L2 misses) run into the
                 // next step
                 auto touches = [&] {
+                    if (rolling) {
+                        const uint32_t pos = E.pos_bytes();
+                        // the stream's first touch starts touch_first windows ahead; later
+                        // ones continue where the last stopped (never behind the position)
+                        touched_to = touched_to == 0 ? pos + touch_first * 8192u : std::max(touched_to, pos);
+                        while (touched_to < pos + (touch_first + troll) * 8192u) {
+                            E.touch_addr(touched_to);
+                            E.nop(4);
+                            E.code_touch(kSinkV, kLane128V);
+                            vm_step++;
+                            touch_step++;
+                            touched_to += 8192u;
+                        }
+                        return;
+                    }
                     for (uint32_t d = 0; d < ntouch; d++) {
                         E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
                         E.nop(4);
@@ -613,6 +643,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     }
                 };
                 vm_step = 0;
+                touch_step = 0;
                 const Section &sec = secs[q];
                 const int nrd = (int)sec.reads.size();
                 const int ngroups = (nrd + G - 1) / G;
@@ -680,7 +711,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         reads_to = std::max(issued, std::min<int64_t>(g1 + RA, first[qm + 1]));
                     }
                     if (!mix_reads) issue_reads(g1 + RA, qra);
-                    if (!mix_dma) pieces_upto(pieces_to);
+                    if (!mix_dma && pieces_to > pieces_out) pieces_upto(pieces_to);
                     const int nr = mix_reads ? (int)(reads_to - issued) : 0;
                     const int np = mix_dma ? pieces_to - pieces_out : 0;
                     const int items = nr + np, na = (int)adds.size();
@@ -723,7 +754,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 }
                 if (lag == 1) {
                     issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
-                    if (!d_novm) E.wait_vm(ntouch);  // this step's pieces (the touches may run on)
+                    if (!d_novm) E.wait_vm(rolling ? touch_step : ntouch);  // this step's pieces (the touches may run on)
                 } else if (!d_novm) {
                     // the previous step's pieces: only its touches and this
                     // step's operations may still be in flight

@@ -715,7 +715,7 @@ def test_jit_code_stagger_and_priority(tsg, oracle_mod, monkeypatch, knobs, M, K
         _check(tsg, oracle_mod, M, K, N, s, 11 + K, frac, width=width, waves=8, rows64=rows64)
 
 
-@pytest.mark.parametrize("mix", ["1,0", "0,1", "1,1"])
+@pytest.mark.parametrize("mix", ["1,0", "0,1", "1,1", "troll=1", "troll=3", "1,1+troll=2"])
 @pytest.mark.parametrize("M,K,N,s,width,waves,rows64", [(130, 400, 520, 4, 64, 8, False), (70, 500, 1100, 4, 128, 8, True),
                                                         (64, 1000, 300, 16, 16, 8, True), (5, 97, 40, 2, 8, 4, True),
                                                         (200, 188, 600, 8, 32, 8, True), (64, 900, 700, 4, 16, 4, True),
@@ -723,10 +723,16 @@ def test_jit_code_stagger_and_priority(tsg, oracle_mod, monkeypatch, knobs, M, K
 def test_jit_code_mixed_issue(tsg, oracle_mod, monkeypatch, mix, M, K, N, s, width, waves, rows64):
     """TSG_JIT_MIX (round 6, A/B): a read group's read-ahead and its share of
     the DMA pieces spread among the group's adds instead of a burst before
-    them.  The emulated workgroup checks every X slot reload against its wait,
+    them; TSG_JIT_TROLL: rolling code touches (each step touches the next
+    untouched 8-KiB windows, the step's closing vmcnt lets exactly those run
+    on).  The emulated workgroup checks every X slot reload against its wait,
     every LDS read against landed pieces and every DMA against reads since its
     issue -- and the result equals the oracle bit for bit."""
-    monkeypatch.setenv("TSG_JIT_MIX", mix)
+    for part in mix.split("+"):
+        if part.startswith("troll="):
+            monkeypatch.setenv("TSG_JIT_TROLL", part[6:])  # rolling code touches (round 6, A/B)
+        else:
+            monkeypatch.setenv("TSG_JIT_MIX", part)
     for frac in (False, True):
         _check(tsg, oracle_mod, M, K, N, s, 13 + K, frac, width=width, waves=waves, rows64=rows64)
 
