@@ -411,6 +411,17 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     uint32_t troll = 0;
     if (const char *tr = knob_value("TSG_JIT_TROLL")) troll = (uint32_t)std::atoi(tr);
     const bool rolling = troll > 0 && ntouch > 0 && !stagger && lag == 1;
+    // TSG_JIT_TGROUP=1|2 (A/B): every read group after a step's last DMA piece
+    // repeats the step's code touch ahead of its own position (1: the step's
+    // closing vmcnt waits for those touches, 2: it lets them run on).  Not
+    // with the stagger, lag 2 or the mixed issue.
+    int tgroup = 0;
+    if (const char *tg = knob_value("TSG_JIT_TGROUP")) tgroup = std::atoi(tg);
+    if (stagger || lag != 1 || mix_dma || ntouch == 0) tgroup = 0;
+    // TSG_JIT_TGAP=bytes: a group repeats the touch only once the code has
+    // advanced at least this far past the previous touch (0: every group)
+    uint32_t tgap = 0;
+    if (const char *tg = knob_value("TSG_JIT_TGAP")) tgap = (uint32_t)std::atoi(tg);
     if (rolling && (touch_first + troll) * 8192u > (uint32_t)kTailPad * 4u) troll = (uint32_t)kTailPad * 4u / 8192u - touch_first;
 
     int n0 = 0;  // first column of the current stream
@@ -477,6 +488,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     };
     int vm_step = 0;  // VMEM operations (DMA pieces, code touches) issued in the current step
     uint32_t touch_step = 0;  // rolling code touches issued in the current step
+    uint32_t extra_touch = 0;  // TSG_JIT_TGROUP touches issued in the current step
+    uint32_t last_touch_pos = 0;  // code position of the last (non-rolling) touch sequence
     uint32_t touched_to = 0;  // rolling: region offset up to which the stream's code is touched
     int cur_wave = 0;  // the wave whose stream is being generated
     auto dma_piece = [&](int q, int i) {
@@ -635,6 +648,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         }
                         return;
                     }
+                    last_touch_pos = E.pos_bytes();
                     for (uint32_t d = 0; d < ntouch; d++) {
                         E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
                         E.nop(4);
@@ -644,6 +658,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 };
                 vm_step = 0;
                 touch_step = 0;
+                extra_touch = 0;
                 const Section &sec = secs[q];
                 const int nrd = (int)sec.reads.size();
                 const int ngroups = (nrd + G - 1) / G;
@@ -711,7 +726,16 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         reads_to = std::max(issued, std::min<int64_t>(g1 + RA, first[qm + 1]));
                     }
                     if (!mix_reads) issue_reads(g1 + RA, qra);
+                    const bool pieces_were_out = dma && pieces_out == kPieces;
                     if (!mix_dma && pieces_to > pieces_out) pieces_upto(pieces_to);
+                    if (tgroup && pieces_were_out && !rolling && extra_touch + ntouch <= 15 - ntouch &&
+                        E.pos_bytes() >= last_touch_pos + tgap) {
+                        // TSG_JIT_TGROUP: every read group after the step's last piece
+                        // touches the code (touch_first .. ) windows ahead of it again
+                        const int before = vm_step;
+                        touches();
+                        extra_touch += (uint32_t)(vm_step - before);
+                    }
                     const int nr = mix_reads ? (int)(reads_to - issued) : 0;
                     const int np = mix_dma ? pieces_to - pieces_out : 0;
                     const int items = nr + np, na = (int)adds.size();
@@ -754,7 +778,8 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 }
                 if (lag == 1) {
                     issue_reads(first[q + 1] + std::max(G, RA), q + 1);  // next step's first reads
-                    if (!d_novm) E.wait_vm(rolling ? touch_step : ntouch);  // this step's pieces (the touches may run on)
+                    if (!d_novm)  // this step's pieces (the touches may run on)
+                        E.wait_vm(rolling ? touch_step : tgroup == 2 ? ntouch + extra_touch : ntouch);
                 } else if (!d_novm) {
                     // the previous step's pieces: only its touches and this
                     // step's operations may still be in flight

@@ -715,7 +715,8 @@ def test_jit_code_stagger_and_priority(tsg, oracle_mod, monkeypatch, knobs, M, K
         _check(tsg, oracle_mod, M, K, N, s, 11 + K, frac, width=width, waves=8, rows64=rows64)
 
 
-@pytest.mark.parametrize("mix", ["1,0", "0,1", "1,1", "troll=1", "troll=3", "1,1+troll=2"])
+@pytest.mark.parametrize("mix", ["1,0", "0,1", "1,1", "troll=1", "troll=3", "1,1+troll=2", "tgroup=1", "tgroup=2",
+                                 "1,0+tgroup=2", "tgroup=2+tgap=4096", "tgroup=1+tgap=1024"])
 @pytest.mark.parametrize("M,K,N,s,width,waves,rows64", [(130, 400, 520, 4, 64, 8, False), (70, 500, 1100, 4, 128, 8, True),
                                                         (64, 1000, 300, 16, 16, 8, True), (5, 97, 40, 2, 8, 4, True),
                                                         (200, 188, 600, 8, 32, 8, True), (64, 900, 700, 4, 16, 4, True),
@@ -731,6 +732,10 @@ def test_jit_code_mixed_issue(tsg, oracle_mod, monkeypatch, mix, M, K, N, s, wid
     for part in mix.split("+"):
         if part.startswith("troll="):
             monkeypatch.setenv("TSG_JIT_TROLL", part[6:])  # rolling code touches (round 6, A/B)
+        elif part.startswith("tgroup="):
+            monkeypatch.setenv("TSG_JIT_TGROUP", part[7:])  # per-group code touches (round 6, A/B)
+        elif part.startswith("tgap="):
+            monkeypatch.setenv("TSG_JIT_TGAP", part[5:])
         else:
             monkeypatch.setenv("TSG_JIT_MIX", part)
     for frac in (False, True):
