@@ -79,6 +79,11 @@ int tcsc_hip_call_far(const tsg_tcsc *h, int M);
 int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int *width, int *waves, int *far,
                   int *gn, int *gm, int *tmask);
 
+/* Whether that call spreads the generated code's per-group code touches over
+ * the stream's lines (1) or points them at one line (0) -- round 6, DESIGN.md
+ * 4.3 "Code touches"; host only.  < 0: TSG_ERR_ARG. */
+int tsg_call_xtouch(int K, int N, int64_t nnz, int M);
+
 /* Machine code of the weight-compiled kernel (TSG_KERNEL=jit) for a TCSC:
  * the generated gfx950 region (uint32 words; region byte offset 0 = word 0)
  * and, per (256-column tile, wave), the byte offset of that wave's stream.

@@ -133,6 +133,7 @@ constexpr double kFarCodeBytes = 160.0 * 1024 * 1024;  // code image well inside
 constexpr double kFarKeepXtBytes = 1536.0 * 1024 * 1024;  // X^T >= 6x it: the far image beats the staged 64-row one
 constexpr double kXDirectMinAddsPerRow = 32.0;  // 64-row image: direct X from width x density >= this
 constexpr int64_t kEllStarvedWgs = 64;
+constexpr double kXTouchMaxXBytes = 384.0 * 1024 * 1024;  // pick_xtouch
 // the 64-row image's step when it cannot read X directly: its X^T staging
 // launch (tsg_transpose_rows_kernel) ahead of the image, at the walk's M
 // (X <= 20 MB) -- r06_staged_floor_ab.jsonl
@@ -531,6 +532,23 @@ bool may_fall_back(const tsg_tcsc *h, const JitShape &sh)
     const bool is_default = !sh.r64 && !sh.far && sh.nw == tsg::kJitNW && sh.waves == tsg::kJitWaves;
     return !is_default && !h->tile_rows && !h->jit_force && h->far_mode != 2 &&
            !tsg::knob_value("TSG_JIT_ROWS64_MAXM") && !tsg::knob_value("TSG_JIT_NW");
+}
+
+// The generated code's per-group code touches (tsg_jit.cpp, round 6: a 128-
+// wide dense stream writes more code per step than the step's one 8-KiB
+// touch covers) run where they were measured to pay: dense W (s <= 2: its
+// steps are ~25 KiB of code), or X of at most 384 MiB (X within ~1.5x the
+// Infinity Cache).  Over long K with large X at s = 4 they cost more than they
+// save (profiles/r06h_tgroup_longk_ab.jsonl, kernel us: (16000, 16384, 4096)
+// 5221 vs 4727 off, (16000, 8192, 2048) 1371 vs 1203; but (4096, 16384, 4096)
+// 1115 vs 1192, configs[2] 1157 vs 1221, (16000, 8192, 2048) s = 2 2152 vs
+// 2394).  Elsewhere the dispatcher points them all at one line.
+// TSG_JIT_XTOUCH=0|1 forces it (A/B, read per call).
+bool pick_xtouch(const tsg_tcsc *h, int M)
+{
+    if (const char *e = tsg::knob_value("TSG_JIT_XTOUCH")) return e[0] == '1';
+    const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
+    return density > 0.375 || 4.0 * (double)M * (double)h->K <= kXTouchMaxXBytes;
 }
 
 JitShape call_shape(const tsg_tcsc *h, int M)
@@ -1014,10 +1032,11 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     int gn = 2, gm = 16, tmask = 0;
     if (h->kind == tsg_tcsc::kJit)
         pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask, r64 ? jv->nw : 0);
+    const int xtouch = pick_xtouch(h, M) ? 1 : 0;
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                jv->nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
-                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0, lastadj)
+                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0, lastadj, xtouch)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)
@@ -1698,6 +1717,22 @@ extern "C" int tsg_call_plan(int K, int N, int64_t nnz, int M, int *kernel, int 
         pick_jit_map(&h, (M + tm - 1) / tm, ntiles, *gn, *gm, *tmask, r64 ? sh.nw : 0);
     }
     return TSG_OK;
+}
+
+// Whether an M-row call of a plain-TCSC handle with K, N and nnz nonzeros
+// spreads the generated code's per-group touches (pick_xtouch; host only).
+extern "C" int tsg_call_xtouch(int K, int N, int64_t nnz, int M)
+{
+    if (K < 0 || N <= 0 || nnz < 0 || nnz > (int64_t)K * N || M <= 0) {
+        g_tsg_host_err = "tsg_call_xtouch: bad arguments";
+        return TSG_ERR_ARG;
+    }
+    tsg_tcsc h;
+    h.K = K;
+    h.N = N;
+    h.nnz_pos = nnz - nnz / 2;
+    h.nnz_neg = nnz / 2;
+    return pick_xtouch(&h, M) ? 1 : 0;
 }
 
 extern "C" const char *tcsc_hip_call_kernel(const tsg_tcsc *h, int M)

@@ -411,16 +411,26 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     uint32_t troll = 0;
     if (const char *tr = knob_value("TSG_JIT_TROLL")) troll = (uint32_t)std::atoi(tr);
     const bool rolling = troll > 0 && ntouch > 0 && !stagger && lag == 1;
-    // TSG_JIT_TGROUP=1|2 (A/B): every read group after a step's last DMA piece
-    // repeats the step's code touch ahead of its own position (1: the step's
-    // closing vmcnt waits for those touches, 2: it lets them run on).  Not
-    // with the stagger, lag 2 or the mixed issue.
-    int tgroup = 0;
+    // Per-group code touches (round 6; TSG_JIT_TGROUP=0|1|2, TSG_JIT_TGAP=
+    // bytes override): a read group after the step's last DMA piece repeats
+    // the step's code touch ahead of its own position once the code has
+    // advanced >= tgap bytes past the previous touch; 2 = the step's closing
+    // vmcnt lets those touches run on (1: it waits for them).  A step's one
+    // 8-KiB touch covers a 16-column stream several steps ahead, but a
+    // 128-wide dense stream writes ~12.6 KiB of code per step at s = 4 (~25
+    // at s = 2): the default (the 64-row image: 2, 4096 B) touches it about
+    // twice per step there and exactly as before for every step of <= 4 KiB
+    // after its last piece.  Measured, kernel us, alternating
+    // (profiles/r06g_tgap_ab.jsonl, r06f_tgroup_ab.jsonl): configs[2]
+    // 1217-1223 -> 1157-1167, s = 2 2309 -> 2177, (1024, 4096, 16384) 309.5
+    // -> 294.8; s = 8 / 16, configs[1] unchanged (same code); with
+    // full-mantissa X configs[2] 1248 vs 1260 (that run is clock-bound).
+    // Every group (gap 0) also slows the short streams: s = 16 +14%,
+    // configs[1] +45%.  Not with the stagger, lag 2 or the mixed DMA issue.
+    int tgroup = r64 ? 2 : 0;
     if (const char *tg = knob_value("TSG_JIT_TGROUP")) tgroup = std::atoi(tg);
     if (stagger || lag != 1 || mix_dma || ntouch == 0) tgroup = 0;
-    // TSG_JIT_TGAP=bytes: a group repeats the touch only once the code has
-    // advanced at least this far past the previous touch (0: every group)
-    uint32_t tgap = 0;
+    uint32_t tgap = 4096;
     if (const char *tg = knob_value("TSG_JIT_TGAP")) tgap = (uint32_t)std::atoi(tg);
     if (rolling && (touch_first + troll) * 8192u > (uint32_t)kTailPad * 4u) troll = (uint32_t)kTailPad * 4u / 8192u - touch_first;
 
@@ -632,7 +642,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 // return in order, so the step's closing vmcnt(ntouch) waits for
                 // every DMA piece but lets the touches (L2 misses) run into the
                 // next step
-                auto touches = [&] {
+                // (lv: the lane-offset VGPR -- v[lane128] for the step's own
+                // touch, v[lane128 + 1] for the per-group ones: the dispatcher
+                // zeroes the latter per call, one line then, tsg_capi.cpp xtouch)
+                auto touches = [&](uint32_t lv) {
                     if (rolling) {
                         const uint32_t pos = E.pos_bytes();
                         // the stream's first touch starts touch_first windows ahead; later
@@ -641,7 +654,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         while (touched_to < pos + (touch_first + troll) * 8192u) {
                             E.touch_addr(touched_to);
                             E.nop(4);
-                            E.code_touch(kSinkV, kLane128V);
+                            E.code_touch(kSinkV, lv);
                             vm_step++;
                             touch_step++;
                             touched_to += 8192u;
@@ -652,7 +665,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                     for (uint32_t d = 0; d < ntouch; d++) {
                         E.touch_addr(E.pos_bytes() + (touch_first + d) * 8192u);
                         E.nop(4);
-                        E.code_touch(kSinkV, kLane128V);
+                        E.code_touch(kSinkV, lv);
                         vm_step++;
                     }
                 };
@@ -673,7 +686,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                 int pieces_out = 0;
                 auto pieces_upto = [&](int upto) {
                     for (; pieces_out < upto; pieces_out++) dma_piece(qd, pieces_out);
-                    if (pieces_out == kPieces && upto == kPieces) touches();
+                    if (pieces_out == kPieces && upto == kPieces) touches(kLane128V);
                 };
                 bool released = !early;  // past this step's barrier (early waves) / after the last one
                 auto dma_start = [&] {
@@ -689,7 +702,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         dma_begin(qd);
                         if (span == 0) pieces_upto(kPieces);
                     } else {
-                        touches();
+                        touches(kLane128V);
                     }
                 };
                 if (!early) dma_start();
@@ -733,7 +746,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                         // TSG_JIT_TGROUP: every read group after the step's last piece
                         // touches the code (touch_first .. ) windows ahead of it again
                         const int before = vm_step;
-                        touches();
+                        touches(kLane128V + 1u);
                         extra_touch += (uint32_t)(vm_step - before);
                     }
                     const int nr = mix_reads ? (int)(reads_to - issued) : 0;
@@ -952,12 +965,13 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream)
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
                     uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask, void *stream,
-                    int tile_m, int xrow, int lastadj)
+                    int tile_m, int xrow, int lastadj, int xtouch)
 {
     int mtiles = Mp / tile_m, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
-                      (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask, (void *)&xrow, (void *)&lastadj};
+                      (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask, (void *)&xrow, (void *)&lastadj,
+                      (void *)&xtouch};
     hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.function, (unsigned)(mtiles * ntiles), 1, 1,
                                          (unsigned)waves * 64u, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;

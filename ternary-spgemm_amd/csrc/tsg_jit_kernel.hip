@@ -33,6 +33,7 @@
 //   v107       code-prefetch sink
 //   v108-113   per-lane byte offsets (from the chunk base) of this wave's 6 LDS-DMA pieces
 //   v114       lane * 128 (code prefetch)
+//   v115       lane * 128 or 0 (the per-group code touches, per call; 4 waves: v121)
 //   v[116:244) accumulators, column c at v116 + 2c (rows 2l, 2l+1 of the lane)
 //   s[80:81] X^T base, s82 chunk stride in bytes, s83 LDS byte offset of this
 //   wave's first DMA piece, s[84:85] chunk base (stream),
@@ -107,13 +108,13 @@ typedef float F32x8 __attribute__((ext_vector_type(8)));
 #if TSG_JIT_WAVES == 8 || TSG_JIT_HALF  // 6 DMA pieces per wave
 #define TSG_JIT_IN                                                                                  \
     "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),             \
-        "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128)
+        "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(l128), "{v115}"(l128x)
 #else
 #define TSG_JIT_IN                                                                                  \
     "{v104}"(lb0), "{v105}"(lb1), "{v106}"(lb2), "{v108}"(off[0]), "{v109}"(off[1]),             \
         "{v110}"(off[2]), "{v111}"(off[3]), "{v112}"(off[4]), "{v113}"(off[5]), "{v114}"(off[6]), \
         "{v115}"(off[7]), "{v116}"(off[8]), "{v117}"(off[9]), "{v118}"(off[10]), "{v119}"(off[11]), \
-        "{v120}"(l128)
+        "{v120}"(l128), "{v121}"(l128x)
 #endif
 
 #define TSG_JIT_CLOBBERS \
@@ -159,7 +160,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
-    int tmask, int xrow, int lastadj)
+    int tmask, int xrow, int lastadj, int xtouch)
 {
     __shared__ __attribute__((aligned(16))) char lds[kJRing * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -253,6 +254,9 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     // load one line 64 times (one request) -- the M tiles that run the same
     // stream share what one of them touched (tsg_capi.cpp pick_jit_map)
     const uint32_t l128 = (mt & tmask) == 0 ? (uint32_t)lane * 128u : 0u;
+    // the generated code's per-group touches (round 6) use v[lane128 + 1]:
+    // the same lines where the call wants them (xtouch), else one line
+    const uint32_t l128x = xtouch ? l128 : 0u;
     // chunk stride: kJChunk K rows of X^T (both staged layouts: Mp * chunk * 4
     // bytes), or of one row-major X row (direct)
     // (row layout: 188-row chunks; the staged copy holds 47 KiB per (chunk, M tile))

@@ -129,6 +129,7 @@ const Knob kKnobs[] = {
     {"TSG_JIT_TOUCH", "first,count (8-KiB units, count <= 4)", touch_ok},
     {"TSG_JIT_READS", "G,RA (G >= 1, G + RA <= 24)", reads_ok},
     {"TSG_JIT_TGROUP", "0 | 1 | 2", [](const char *v) { return one_of(v, {"0", "1", "2"}); }},
+    {"TSG_JIT_XTOUCH", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_TGAP", "0..65536 (bytes)", [](const char *v) { return int_in(v, 0, 65536); }},
     {"TSG_JIT_TROLL", "0..8 (rolling code touches, 8-KiB windows ahead)", [](const char *v) { return int_in(v, 0, 8); }},
     {"TSG_JIT_MIX", "reads,dma (0|1 each)",

@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "tcsc_hip_set_small_m", "tcsc_hip_call_kernel", "tsg_ell_build", "tsg_jit_tile_map",
     "tcsc_hip_set_host_chunks", "tcsc_hip_host_chunk_rows", "tcsc_hip_call_image_bytes",
     "tcsc_hip_host_register", "tcsc_hip_host_unregister", "tcsc_hip_set_far", "tcsc_hip_call_far",
-    "tsg_jit_codegen_far", "tsg_call_plan", "tsg_knob_check", "tcsc_hip_set_tile_rows", "tcsc_hip_call_tile_rows",
+    "tsg_jit_codegen_far", "tsg_call_plan", "tsg_call_xtouch", "tsg_knob_check", "tcsc_hip_set_tile_rows", "tcsc_hip_call_tile_rows",
     "tsg_jit_codegen64", "tsg_jit_codegen64h", "tcsc_hip_call_launches",
 )
 
@@ -139,6 +139,7 @@ def lib() -> C.CDLL:
     L.tsg_jit_codegen64h.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                      C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
     L.tsg_call_plan.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int] + [C.POINTER(C.c_int)] * 7
+    L.tsg_call_xtouch.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int]
     L.tcsc_hip_call_far.argtypes = [H, C.c_int]
     L.tsg_jit_codegen_far.argtypes = [vp, vp, vp, vp, C.c_int, C.c_int, vp, C.c_int64,
                                       C.POINTER(C.c_int64), vp, C.c_int64, C.POINTER(C.c_int64)]
@@ -327,6 +328,14 @@ def call_plan(K: int, N: int, nnz: int, M: int) -> dict:
     kernel, width, waves, far, gn, gm, tmask = (x.value for x in v)
     return {"kernel": ("tsg_jit_kernel", "tsg_tcsc_ell_kernel", "tsg_tcsc_ell_pc_kernel", "tsg_jit64_kernel")[kernel],
             "width": width, "waves": waves, "far": bool(far), "map": (gn, gm), "tmask": tmask}
+
+
+def call_xtouch(K: int, N: int, nnz: int, M: int) -> bool:
+    """Whether an M-row call spreads the generated code's per-group code
+    touches over the lines (tsg_call_xtouch, host only)."""
+    r = lib().tsg_call_xtouch(K, N, nnz, M)
+    _check(min(r, 0), "tsg_call_xtouch")
+    return bool(r)
 
 
 def jit_tile_map(L: int, mtiles: int, ntiles: int, gn: int, gm: int):

@@ -190,3 +190,18 @@ def test_plan_x_past_32bit_offsets_keeps_round4_rules(tsg):
 ])
 def test_plan_staged_image_rules(tsg, M, K, N, kernel):
     assert tsg.call_plan(K, N, K * N // 4, M)["kernel"] == kernel
+
+
+@pytest.mark.parametrize("M,K,N,s,on", [
+    # the per-group code touches spread (tsg_capi.cpp pick_xtouch; profiles/r06h_tgroup_longk_ab.jsonl)
+    (4096, 4096, 16384, 4, True),     # configs[2] 1157 vs 1221 us
+    (4096, 4096, 16384, 2, True),     # s = 2 2177 vs 2309
+    (4096, 16384, 4096, 4, True),     # 1115 vs 1192
+    (16000, 8192, 2048, 2, True),     # dense: 2152 vs 2394
+    (64000, 16384, 4096, 2, True),    # 34.3 vs 38.0 ms (r06a_ref_cases.jsonl)
+    (16000, 8192, 2048, 4, False),    # 1203 vs 1371
+    (16000, 16384, 4096, 4, False),   # 4727 vs 5221
+    (64000, 16384, 4096, 4, False),   # 18.9 vs 24.4 ms
+])
+def test_plan_xtouch(tsg, M, K, N, s, on):
+    assert tsg.call_xtouch(K, N, K * N // s, M) is on

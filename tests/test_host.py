@@ -156,7 +156,7 @@ def test_drop_in_header_is_the_product_surface():
               "tcsc_hip_reserve", "tcsc_hip_last_error"):
         assert f in product
     for f in ("tcsc_hip_set_jit_width", "tcsc_hip_set_small_m", "tcsc_hip_set_far", "tsg_jit_codegen_wv",
-              "tsg_call_plan", "tsg_jit_tile_map", "tsg_ell_build", "tsg_knob_check"):
+              "tsg_call_plan", "tsg_call_xtouch", "tsg_jit_tile_map", "tsg_ell_build", "tsg_knob_check"):
         assert f in hooks
 
 

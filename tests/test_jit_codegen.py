@@ -140,7 +140,8 @@ def _decode(code, pc, G):
         return "touch_addr", (w1,), 2
     CP = 0x2030000  # cache-policy bits (sc0, nt, sc1): any combination
     if (w0 & ~CP) == 0xDC508000:
-        assert w1 == (G.sink_v << 24) | (88 << 16) | G.l128_v
+        # the step's own touch: v[lane128]; the per-group ones (round 6): v[lane128 + 1]
+        assert w1 in ((G.sink_v << 24) | (88 << 16) | G.l128_v, (G.sink_v << 24) | (88 << 16) | (G.l128_v + 1))
         return "touch", (), 2
     if (w0 & ~CP & 0xFFFFF000) == 0xDDF48000:  # global_load_lds_dwordx4 v, s[84:85] offset:(w0 & 0xFFF)
         assert (w1 >> 16) == 84
