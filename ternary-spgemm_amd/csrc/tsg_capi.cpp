@@ -133,7 +133,8 @@ constexpr double kFarCodeBytes = 160.0 * 1024 * 1024;  // code image well inside
 constexpr double kFarKeepXtBytes = 1536.0 * 1024 * 1024;  // X^T >= 6x it: the far image beats the staged 64-row one
 constexpr double kXDirectMinAddsPerRow = 32.0;  // 64-row image: direct X from width x density >= this
 constexpr int64_t kEllStarvedWgs = 64;
-constexpr double kXTouchMaxXBytes = 384.0 * 1024 * 1024;  // pick_xtouch
+constexpr double kXTouchMaxXBytes = 384.0 * 1024 * 1024;        // pick_xtouch
+constexpr double kXTouchDenseMaxXBytes = 1024.0 * 1024 * 1024;  // (dense W)
 // the 64-row image's step when it cannot read X directly: its X^T staging
 // launch (tsg_transpose_rows_kernel) ahead of the image, at the walk's M
 // (X <= 20 MB) -- r06_staged_floor_ab.jsonl
@@ -536,19 +537,21 @@ bool may_fall_back(const tsg_tcsc *h, const JitShape &sh)
 
 // The generated code's per-group code touches (tsg_jit.cpp, round 6: a 128-
 // wide dense stream writes more code per step than the step's one 8-KiB
-// touch covers) run where they were measured to pay: dense W (s <= 2: its
-// steps are ~25 KiB of code), or X of at most 384 MiB (X within ~1.5x the
-// Infinity Cache).  Over long K with large X at s = 4 they cost more than they
-// save (profiles/r06h_tgroup_longk_ab.jsonl, kernel us: (16000, 16384, 4096)
-// 5221 vs 4727 off, (16000, 8192, 2048) 1371 vs 1203; but (4096, 16384, 4096)
-// 1115 vs 1192, configs[2] 1157 vs 1221, (16000, 8192, 2048) s = 2 2152 vs
-// 2394).  Elsewhere the dispatcher points them all at one line.
-// TSG_JIT_XTOUCH=0|1 forces it (A/B, read per call).
+// touch covers) run where they were measured to pay: X of at most 384 MiB
+// (~1.5x the Infinity Cache), and dense W (s <= 2: steps of ~25 KiB of code)
+// with X up to 1 GiB.  With large X they cost more than they save
+// (profiles/r06h_tgroup_longk_ab.jsonl, kernel us: (16000, 16384, 4096) s = 4
+// 5221 vs 4727 off, (16000, 8192, 2048) s = 4 1371 vs 1203;
+// r06i_xtouch_big_ab.jsonl: (64000, 16384, 4096) s = 2 34.2-46.5 ms, unsteady,
+// vs 38.0-38.4 off) -- but (4096, 16384, 4096) 1115 vs 1192, configs[2] 1157
+// vs 1221, (16000, 8192, 2048) s = 2 2152 vs 2394.  Elsewhere the dispatcher
+// points them all at one line.  TSG_JIT_XTOUCH=0|1 forces it (A/B, per call).
 bool pick_xtouch(const tsg_tcsc *h, int M)
 {
     if (const char *e = tsg::knob_value("TSG_JIT_XTOUCH")) return e[0] == '1';
     const double density = (double)(h->nnz_pos + h->nnz_neg) / std::max(1.0, (double)h->K * (double)h->N);
-    return density > 0.375 || 4.0 * (double)M * (double)h->K <= kXTouchMaxXBytes;
+    const double xbytes = 4.0 * (double)M * (double)h->K;
+    return xbytes <= kXTouchMaxXBytes || (density > 0.375 && xbytes <= kXTouchDenseMaxXBytes);
 }
 
 JitShape call_shape(const tsg_tcsc *h, int M)

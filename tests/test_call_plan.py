@@ -198,7 +198,7 @@ def test_plan_staged_image_rules(tsg, M, K, N, kernel):
     (4096, 4096, 16384, 2, True),     # s = 2 2177 vs 2309
     (4096, 16384, 4096, 4, True),     # 1115 vs 1192
     (16000, 8192, 2048, 2, True),     # dense: 2152 vs 2394
-    (64000, 16384, 4096, 2, True),    # 34.3 vs 38.0 ms (r06a_ref_cases.jsonl)
+    (64000, 16384, 4096, 2, False),   # X 4.2 GB: 34.2-46.5 ms unsteady vs 38.0-38.4 (r06i_xtouch_big_ab.jsonl)
     (16000, 8192, 2048, 4, False),    # 1203 vs 1371
     (16000, 16384, 4096, 4, False),   # 4727 vs 5221
     (64000, 16384, 4096, 4, False),   # 18.9 vs 24.4 ms
