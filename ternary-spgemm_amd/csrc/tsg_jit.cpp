@@ -393,8 +393,14 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     constexpr bool d_nobar = false, d_nodma = false, d_notouch = false, d_nolgkm = false, d_noreads = false,
                    d_novm = false;
 #endif
-    // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default 1,1)
-    uint32_t touch_first = 1, touch_count = 1;
+    // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default
+    // 1,1; the 64-row image's 4-wave workgroups 0,1: the 8 KiB from the step's
+    // own position -- their one-M-tile calls stream each code line once, from
+    // HBM, and the nearer window pays there: M = 64 / 48 at K = 4096, N =
+    // 16384 58.9 / 57.4 -> 51.7 / 50.0 us, (64, 2048, 8192) s = 2 32.1 ->
+    // 28.6, (1024, 4096, 1024) 56.1 -> 54.9; with several M tiles a tie, and
+    // the 8-wave shapes +1% (profiles/r06j_touch_small_ab.jsonl))
+    uint32_t touch_first = r64 && waves == 4 ? 0u : 1u, touch_count = 1;
     if (const char *tv = knob_value("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
     if (touch_count > 4) touch_count = 4;
     // the prefetch must stay inside the tail padding past the last stream
