@@ -50,7 +50,7 @@ import tspgemm as T  # noqa: E402
 import tsg_dist as D  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak (spec)
-PROFILE_PMC = os.path.join(REPO, "profiles", "r05final5_pmc_summary.json")
+PROFILE_PMC = os.path.join(REPO, "profiles", "r06final_pmc_summary.json")
 # Binding roof of the path: fp32 VALU adds.  v_pk_add_f32 retires 2 IEEE adds per
 # lane, 128 adds/clk/CU (measured 121 in scripts/issue_micro.hip), x 256 CUs x
 # 2.4 GHz = 78.6 T adds/s (the 157.3 TFLOP/s fp32 vector spec counts an FMA as 2).
