@@ -23,7 +23,7 @@ def classify(code, i):
         return "dma", 2
     if w0 == 0xDC508000:
         return "touch", 2
-    if w0 in (0x807CFF53, 0x8058FF5C):
+    if w0 in (0x807CFF53, 0x8058FF5A):
         return "salu_lit", 2
     if w0 == 0xBF800000:
         return "pad_nop0", 1

@@ -554,6 +554,23 @@ bool pick_xtouch(const tsg_tcsc *h, int M)
     return xbytes <= kXTouchMaxXBytes || (density > 0.375 && xbytes <= kXTouchDenseMaxXBytes);
 }
 
+// The code-touch window (tsg_jit.cpp: 8 KiB, from 8 KiB ahead of the step's
+// position) starts at the step's own position instead -- the dispatcher
+// moves the touch base back 8 KiB -- for 64-row calls with at most 2 M
+// tiles, and on 4-wave workgroups: with few M tiles each code line is
+// fetched by few workgroups, much of it straight from HBM, and the nearer
+// window pays (profiles/r06j_touch_small_ab.jsonl, r06p_touch_8w_ab.jsonl,
+// kernel us: M = 64 / 48, N = 16384 (16 x 4) 58.9 / 57.4 -> 51.7 / 50.0,
+// M = 128 (16 x 8, 2 M tiles) 74.3 -> 64.4, (64, 2048, 8192) s = 2 32.1 ->
+// 28.6, (1024, 4096, 1024) (16 x 4) 56.1 -> 54.9; M = 192 (3 tiles) -1%,
+// configs[1] (8 tiles) +1%, (256, 4096, 8192) a tie).  TSG_JIT_TNEAR=0|1
+// forces it (A/B, read per call).
+bool pick_tnear(bool r64, int waves, int mtiles)
+{
+    if (const char *e = tsg::knob_value("TSG_JIT_TNEAR")) return e[0] == '1';
+    return r64 && (mtiles <= 2 || waves == 4);
+}
+
 JitShape call_shape(const tsg_tcsc *h, int M)
 {
     const JitShape sh = pick_jit_shape(h, M, pick_rows64(h, M));
@@ -1036,10 +1053,11 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     if (h->kind == tsg_tcsc::kJit)
         pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask, r64 ? jv->nw : 0);
     const int xtouch = pick_xtouch(h, M) ? 1 : 0;
+    const int tnear = pick_tnear(r64, jv->waves, Mp / tile_m) ? 1 : 0;
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                jv->nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
-                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0, lastadj, xtouch)
+                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0, lastadj, xtouch, tnear)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)

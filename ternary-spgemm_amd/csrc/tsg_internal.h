@@ -216,11 +216,13 @@ struct JitModule {
 };
 // xrow > 0: the 64-row image stages straight from X (xrow floats per row);
 // lastadj: bytes the row layout's last chunk starts below its slot (direct X);
-// xtouch: the per-group code touches (v[lane128 + 1]) spread over the lines
+// xtouch: the per-group code touches (v[lane128 + 1]) spread over the lines;
+// tnear: the code touches' window starts at the step's own position
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode,
                     const float *b, const float *alpha, float *Y, int M, int N, int Npad, int nch,
                     int prelu, uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask,
-                    void *stream, int tile_m = kJitTileM, int xrow = 0, int lastadj = 0, int xtouch = 0);
+                    void *stream, int tile_m = kJitTileM, int xrow = 0, int lastadj = 0, int xtouch = 0,
+                    int tnear = 0);
 int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream);
 
 // ---------------------------------------------------------------------------

@@ -122,12 +122,15 @@ struct Emit {
         c.push_back(0x80d45754u);
         c.push_back(0x82d58055u);
     }
-    void touch_addr(uint32_t region_off)              // s[88:89] = s[92:93] + off
+    // s[88:89] = s[90:91] + off: s[90:91] is the touch base the dispatcher
+    // sets per call -- the region base, or 8 KiB below it (the touches then
+    // cover the code from the step's own position, tsg_capi.cpp tnear)
+    void touch_addr(uint32_t region_off)
     {
         align8();
-        c.push_back(0x8058ff5cu);
+        c.push_back(0x8058ff5au);
         c.push_back(region_off);
-        c.push_back(0x8259805du);
+        c.push_back(0x8259805bu);
     }
     void nop(uint32_t n = 0) { c.push_back(0xbf800000u | n); }
     void wait_lgkm(uint32_t n) { c.push_back(0xbf8cc07fu | (n << 8)); }  // s_waitcnt lgkmcnt(n), n <= 15
@@ -394,13 +397,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
                    d_novm = false;
 #endif
     // code-prefetch window: TSG_JIT_TOUCH="first,count" in 8-KiB units (default
-    // 1,1; the 64-row image's 4-wave workgroups 0,1: the 8 KiB from the step's
-    // own position -- their one-M-tile calls stream each code line once, from
-    // HBM, and the nearer window pays there: M = 64 / 48 at K = 4096, N =
-    // 16384 58.9 / 57.4 -> 51.7 / 50.0 us, (64, 2048, 8192) s = 2 32.1 ->
-    // 28.6, (1024, 4096, 1024) 56.1 -> 54.9; with several M tiles a tie, and
-    // the 8-wave shapes +1% (profiles/r06j_touch_small_ab.jsonl))
-    uint32_t touch_first = r64 && waves == 4 ? 0u : 1u, touch_count = 1;
+    // 1,1), relative to the touch base s[90:91]: the dispatcher moves it 8 KiB
+    // back per call (the window then starts at the step's own position) where
+    // that pays (tsg_capi.cpp pick_tnear)
+    uint32_t touch_first = 1, touch_count = 1;
     if (const char *tv = knob_value("TSG_JIT_TOUCH")) std::sscanf(tv, "%u,%u", &touch_first, &touch_count);
     if (touch_count > 4) touch_count = 4;
     // the prefetch must stay inside the tail padding past the last stream
@@ -971,13 +971,13 @@ int launch_jit_probe(const JitModule &jm, uint32_t *status, void *stream)
 int launch_tcsc_jit(const JitModule &jm, const float *XT, int Mp, const uint32_t *wcode, const float *b,
                     const float *alpha, float *Y, int M, int N, int Npad, int nch, int prelu,
                     uint32_t *status, int tile_cols, int waves, int gn, int gm, int tmask, void *stream,
-                    int tile_m, int xrow, int lastadj, int xtouch)
+                    int tile_m, int xrow, int lastadj, int xtouch, int tnear)
 {
     int mtiles = Mp / tile_m, ntiles = Npad / tile_cols;
     void *params[] = {(void *)&XT, (void *)&Mp, (void *)&wcode, (void *)&b, (void *)&alpha, (void *)&Y,
                       (void *)&M, (void *)&N, (void *)&nch, (void *)&mtiles, (void *)&ntiles, (void *)&prelu,
                       (void *)&status, (void *)&gn, (void *)&gm, (void *)&tmask, (void *)&xrow, (void *)&lastadj,
-                      (void *)&xtouch};
+                      (void *)&xtouch, (void *)&tnear};
     hipError_t e = hipModuleLaunchKernel((hipFunction_t)jm.function, (unsigned)(mtiles * ntiles), 1, 1,
                                          (unsigned)waves * 64u, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     return e == hipSuccess ? 0 : -1;

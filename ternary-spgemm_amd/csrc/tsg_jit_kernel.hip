@@ -39,6 +39,7 @@
 //   wave's first DMA piece, s[84:85] chunk base (stream),
 //   s86 saved M0, s87 bytes the 64-row row layout's last chunk starts below
 //   its slot (direct X; else 0), s[88:89] prefetch address (stream),
+//   s[90:91] code-touch base (region base, or 8 KiB below it per call),
 //   s[92:93] region base, s[94:95] return address.
 #include <hip/hip_runtime.h>
 
@@ -160,7 +161,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
-    int tmask, int xrow, int lastadj, int xtouch)
+    int tmask, int xrow, int lastadj, int xtouch, int tnear)
 {
     __shared__ __attribute__((aligned(16))) char lds[kJRing * kJBufBytes];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -257,6 +258,11 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     // the generated code's per-group touches (round 6) use v[lane128 + 1]:
     // the same lines where the call wants them (xtouch), else one line
     const uint32_t l128x = xtouch ? l128 : 0u;
+    // the code touches' base (s[90:91]): the region base, or 8 KiB below it
+    // for calls whose touch window should start at the step's own position
+    // (tnear; the generated code never touches less than 8 KiB ahead of its
+    // position relative to this base, so the window stays inside the region)
+    const uint64_t tbase = base - (tnear ? 8192u : 0u);
     // chunk stride: kJChunk K rows of X^T (both staged layouts: Mp * chunk * 4
     // bytes), or of one row-major X row (direct)
     // (row layout: 188-row chunks; the staged copy holds 47 KiB per (chunk, M tile))
@@ -273,7 +279,8 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
                  "s_setpc_b64 %[cp]\n"                                                              \
                  ".Ljb%=:"                                                                          \
                  : __VA_ARGS__                                                                      \
-                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[80:81]}"(xbase), "{s82}"(stride), "{s83}"(wb), "{s87}"(adj), \
+                 : [cp] "s"(cp), "{s[92:93]}"(base), "{s[90:91]}"(tbase), "{s[80:81]}"(xbase), "{s82}"(stride),  \
+                   "{s83}"(wb), "{s87}"(adj),                                                          \
                    TSG_JIT_IN                                                                       \
                  : TSG_JIT_CLOBBERS)
 #if TSG_JIT_ROWS64  // one accumulator VGPR per column (acc0 = v116; 4 waves: v122, half ring v116)

@@ -75,11 +75,13 @@ bool cp_ok(const char *v)
     return true;
 }
 
-// TSG_JIT_TOUCH = "first,count" in 8-KiB units, count <= 4, inside the tail padding
+// TSG_JIT_TOUCH = "first,count" in 8-KiB units, first >= 1 (the dispatcher may
+// move the touch base 8 KiB back, tsg_capi.cpp pick_tnear), count <= 4, inside
+// the tail padding
 bool touch_ok(const char *v)
 {
     const auto f = fields(v);
-    if (f.size() != 2 || !parse_i64(f[0], 0, 64) || !parse_i64(f[1], 0, 4)) return false;
+    if (f.size() != 2 || !parse_i64(f[0], 1, 64) || !parse_i64(f[1], 0, 4)) return false;
     return (std::atoll(f[0].c_str()) + std::atoll(f[1].c_str())) * 8192ll <= (int64_t)kJitTailPadWords * 4;
 }
 
@@ -126,10 +128,11 @@ const Knob kKnobs[] = {
     {"TSG_JIT_TMASK", "0..255", [](const char *v) { return int_in(v, 0, 255); }},
     {"TSG_JIT_DMA", "spread[0..1],m0k[0|1][,lag[1|2]]", dma_ok},
     {"TSG_JIT_CP", "dma,touch (hex, bits of 0x2030000)", cp_ok},
-    {"TSG_JIT_TOUCH", "first,count (8-KiB units, count <= 4)", touch_ok},
+    {"TSG_JIT_TOUCH", "first,count (8-KiB units, first >= 1, count <= 4)", touch_ok},
     {"TSG_JIT_READS", "G,RA (G >= 1, G + RA <= 24)", reads_ok},
     {"TSG_JIT_TGROUP", "0 | 1 | 2", [](const char *v) { return one_of(v, {"0", "1", "2"}); }},
     {"TSG_JIT_XTOUCH", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
+    {"TSG_JIT_TNEAR", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_TGAP", "0..65536 (bytes)", [](const char *v) { return int_in(v, 0, 65536); }},
     {"TSG_JIT_TROLL", "0..8 (rolling code touches, 8-KiB windows ahead)", [](const char *v) { return int_in(v, 0, 8); }},
     {"TSG_JIT_MIX", "reads,dma (0|1 each)",

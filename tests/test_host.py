@@ -171,6 +171,7 @@ def _small_tcsc(oracle_mod):
     ("TSG_JIT_DMA", "0.5;1", "TSG_JIT_DMA=0.5;1: expected"),
     ("TSG_JIT_DMA", "2,1", "expected"),                  # spread outside [0, 1]
     ("TSG_JIT_TOUCH", "1,9", "expected"),
+    ("TSG_JIT_TOUCH", "0,1", "expected"),  # first >= 1: the per-call near bias would reach before the region
     ("TSG_JIT_READS", "20,20", "expected"),
     ("TSG_JIT_CP", "0x40,0", "expected"),
     ("TSG_JIT_GN", "two", "expected"),

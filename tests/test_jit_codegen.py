@@ -131,12 +131,15 @@ def _decode(code, pc, G):
         return "wait_vm", (w0 & 0xF,), 1
     simple = {0xBF8A0000: "barrier", 0xBED6007C: "save_m0", 0x80D45754: "last_adj", 0x82D58055: "last_adjc",
               0xBEFC0056: "restore_m0", 0xBED40150: "base_reset", 0xBE801D5E: "ret", 0x82558055: "base_addc",
-              0x8259805D: "touch_addc", 0x80545254: "base_add"}
+              0x8259805B: "touch_addc", 0x80545254: "base_add"}
     if w0 in simple:
         return simple[w0], (), 1
     if w0 == 0x807CFF53:  # s_add_u32 m0, s83, lit
         return "m0", (w1,), 2
-    if w0 == 0x8058FF5C:
+    if w0 == 0x8058FF5A:  # s_add_u32 s88, s90, lit: the touch base s[90:91] (region base or 8 KiB below)
+        # never less than 8 KiB ahead relative to the base: with the dispatcher's
+        # near bias (-8 KiB) the touch still starts inside the region
+        assert w1 >= 8192, "code touch closer than 8 KiB to the touch base"
         return "touch_addr", (w1,), 2
     CP = 0x2030000  # cache-policy bits (sc0, nt, sc1): any combination
     if (w0 & ~CP) == 0xDC508000:
@@ -576,7 +579,7 @@ def _count_entry_adds(code, G):
         if (w0 & 0xFFFFFC00) == 0xD3B24000 and (int(code[i + 1]) >> 27) & 3 == 3:
             n += _classify_pk(w0, int(code[i + 1]), G)[0] in ("add", "first")
             i += 2
-        elif w0 in (0x807CFF53, 0x8058FF5C) or (w0 >> 26) in (0x36, 0x37) or (w0 >> 24) == 0xDD or (w0 >> 24) == 0xDC:
+        elif w0 in (0x807CFF53, 0x8058FF5A) or (w0 >> 26) in (0x36, 0x37) or (w0 >> 24) == 0xDD or (w0 >> 24) == 0xDC:
             i += 2  # literal SALU, DS, global / LDS-DMA: 8 bytes
         else:
             i += 1
