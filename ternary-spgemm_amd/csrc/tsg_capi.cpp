@@ -1052,8 +1052,10 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     int gn = 2, gm = 16, tmask = 0;
     if (h->kind == tsg_tcsc::kJit)
         pick_jit_map(h, Mp / tile_m, jv->Npad / (jv->nw * jv->waves), gn, gm, tmask, r64 ? jv->nw : 0);
-    const int xtouch = pick_xtouch(h, M) ? 1 : 0;
-    const int tnear = pick_tnear(r64, jv->waves, Mp / tile_m) ? 1 : 0;
+    // (jv is null on the rx kernel)
+    const bool jit = h->kind == tsg_tcsc::kJit;
+    const int xtouch = jit && pick_xtouch(h, M) ? 1 : 0;
+    const int tnear = jit && pick_tnear(r64, jv->waves, Mp / tile_m) ? 1 : 0;
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                jv->nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
