@@ -245,6 +245,85 @@ std::vector<StepSpec> plan_steps(int K, int N, int B, int nch, int nw, int C = k
 
 }  // namespace
 
+#ifdef TSG_DIAG
+// Column -> wave assignment of one column tile that evens out the waves'
+// per-step work (round 6, diagnostic build only; measured no faster --
+// configs[1] 59.6 vs 59.4 us, s = 16 428.4 vs 430.0, configs[2] +3%; even
+// piling the heaviest columns on the first waves changes nothing:
+// profiles/r06s_balance_diag.jsonl -- the per-step barrier costs its sync,
+// not the waves' imbalance): every step ends in a workgroup
+// barrier, so a step lasts as long as its busiest wave.  The tile's columns
+// move between waves in units of `unit` consecutive columns (4 keeps the
+// epilogue's float4 stores); a local search swaps units between waves while
+// the sum over steps of the busiest wave's entries does not grow.  perm[w *
+// nw + c] = the tile-local column the wave's accumulator c holds.
+std::vector<int> balance_tile(const int32_t *csp, const int32_t *csn, const int32_t *rip, const int32_t *rin,
+                              int N, int n_tile0, int tile_cols, int waves, int nw, int CH, int nch, int unit,
+                              bool anti)
+{
+    const int steps = 2 * nch, units = tile_cols / unit, upw = nw / unit;
+    std::vector<int64_t> V((size_t)units * steps, 0);  // entries per (unit, step)
+    for (int p = 0; p < 2; p++) {
+        const int32_t *cs = p ? csn : csp, *ri = p ? rin : rip;
+        for (int cl = 0; cl < tile_cols; cl++) {
+            const int n = n_tile0 + cl;
+            if (n >= N) continue;
+            for (int32_t i = cs[n]; i < cs[n + 1]; i++)
+                V[(size_t)(cl / unit) * steps + p * nch + std::min(ri[i] / CH, nch - 1)]++;
+        }
+    }
+    std::vector<int> g(units);  // g[w * upw + j] = unit
+    for (int u = 0; u < units; u++) g[u] = u;
+    if (anti) {  // the heaviest units on the first waves
+        std::vector<int64_t> tot(units, 0);
+        for (int u = 0; u < units; u++)
+            for (int q = 0; q < steps; q++) tot[u] += V[(size_t)u * steps + q];
+        std::stable_sort(g.begin(), g.end(), [&](int a, int b) { return tot[a] > tot[b]; });
+    } else if (waves > 1) {
+        std::vector<int64_t> S((size_t)waves * steps, 0);
+        for (int w = 0; w < waves; w++)
+            for (int j = 0; j < upw; j++)
+                for (int q = 0; q < steps; q++) S[(size_t)w * steps + q] += V[(size_t)g[w * upw + j] * steps + q];
+        uint64_t rng = 0x9E3779B97F4A7C15ull ^ (uint64_t)n_tile0;
+        auto rnd = [&](int m) {
+            rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+            return (int)(rng % (uint64_t)m);
+        };
+        const int iters = 40 * units * waves;
+        std::vector<int64_t> others(steps);
+        for (int it = 0; it < iters; it++) {
+            const int a = rnd(waves), b0 = rnd(waves - 1), b = b0 >= a ? b0 + 1 : b0;
+            const int i = rnd(upw), j = rnd(upw);
+            const int ua = g[a * upw + i], ub = g[b * upw + j];
+            int64_t dcost = 0;
+            for (int q = 0; q < steps; q++) {
+                int64_t mo = 0;
+                for (int w = 0; w < waves; w++)
+                    if (w != a && w != b) mo = std::max(mo, S[(size_t)w * steps + q]);
+                const int64_t d = V[(size_t)ub * steps + q] - V[(size_t)ua * steps + q];
+                const int64_t sa = S[(size_t)a * steps + q], sb = S[(size_t)b * steps + q];
+                dcost += std::max(mo, std::max(sa + d, sb - d)) - std::max(mo, std::max(sa, sb));
+            }
+            if (dcost <= 0) {
+                for (int q = 0; q < steps; q++) {
+                    const int64_t d = V[(size_t)ub * steps + q] - V[(size_t)ua * steps + q];
+                    S[(size_t)a * steps + q] += d;
+                    S[(size_t)b * steps + q] -= d;
+                }
+                g[a * upw + i] = ub;
+                g[b * upw + j] = ua;
+            }
+        }
+        for (int w = 0; w < waves; w++) std::sort(g.begin() + w * upw, g.begin() + (w + 1) * upw);
+    }
+    std::vector<int> perm(tile_cols);
+    for (int w = 0; w < waves; w++)
+        for (int j = 0; j < upw; j++)
+            for (int e = 0; e < unit; e++) perm[w * nw + j * unit + e] = g[w * upw + j] * unit + e;
+    return perm;
+}
+#endif
+
 int jit64_piece_rows()
 {
     const char *v = knob_value("TSG_JIT_QBLOCK");
@@ -441,6 +520,17 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     if (rolling && (touch_first + troll) * 8192u > (uint32_t)kTailPad * 4u) troll = (uint32_t)kTailPad * 4u / 8192u - touch_first;
 
     int n0 = 0;  // first column of the current stream
+    int tile0 = 0, slot0 = 0;  // first column of the tile, the wave's first slot in tile_perm
+    std::vector<int> tile_perm(tile_cols);  // accumulator slot -> tile-local column
+    for (int i = 0; i < tile_cols; i++) tile_perm[i] = i;
+#ifdef TSG_DIAG
+    // TSG_JIT_DIAG=balance4|balance1|anti4 (results WRONG: the dispatcher
+    // still writes accumulator c of wave w to column w * nw + c): the
+    // timing of a balanced / unbalanced column -> wave assignment
+    const int d_bal = has("balance4") ? 4 : has("balance1") ? 1 : has("anti4") ? -4 : 0;
+#else
+    constexpr int d_bal = 0;
+#endif
     std::vector<int32_t> cur((size_t)nw * 2), end((size_t)nw * 2);
     std::vector<uint8_t> live(nw, 0);  // BlockedTCSC: y of the column holds an entry
     // step q's section: the wave's entries in rows [klo, khi) of its pass, as
@@ -453,7 +543,7 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
         const int32_t *cs = p ? csn : csp, *ri = p ? rin : rip;
         if (sp.reset)
             for (int col = sp.c0; col < sp.c1; col++) {
-                const int n = n0 + col;
+                const int n = d_bal ? tile0 + tile_perm[slot0 + col] : n0 + col;
                 cur[(size_t)col * 2 + p] = n < N ? cs[sp.slot0 + n] : 0;
                 end[(size_t)col * 2 + p] = n < N ? cs[sp.slot0 + n + 1] : 0;
             }
@@ -562,6 +652,13 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
             img.wcode[(size_t)t * streams + w] = E.pos_bytes();
             cur_wave = w;
             n0 = t * tile_cols + w * nw;
+            tile0 = t * tile_cols;
+            slot0 = w * nw;
+#ifdef TSG_DIAG
+            if (d_bal && w == 0 && !B && nw % 4 == 0)
+                tile_perm = balance_tile(csp, csn, rip, rin, N, tile0, tile_cols, waves, nw, CH, nch,
+                                         d_bal < 0 ? -d_bal : d_bal, d_bal < 0);
+#endif
             std::fill(live.begin(), live.end(), 0);
             base_chunk = -1;
             touched_to = 0;

@@ -99,7 +99,7 @@ bool diag_ok(const char *v)
 {
     for (const auto &s : fields(v))
         if (!one_of(s.c_str(), {"nobar", "nodma", "notouch", "nolgkm", "noreads", "novm", "samecode", "samewave",
-                                "pairwave", "simdpair"}))
+                                "pairwave", "simdpair", "balance4", "balance1", "anti4"}))
             return false;
     return true;
 }
@@ -149,7 +149,7 @@ const Knob kKnobs[] = {
     {"TSG_ELL_WPG", "4 | 8 | 16", [](const char *v) { return one_of(v, {"4", "8", "16"}); }},
     {"TSG_ELL_SCHED", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
 #ifdef TSG_DIAG
-    {"TSG_JIT_DIAG", "nobar,nodma,notouch,nolgkm,noreads,novm,samecode,samewave,pairwave,simdpair", diag_ok},
+    {"TSG_JIT_DIAG", "nobar,nodma,notouch,nolgkm,noreads,novm,samecode,samewave,pairwave,simdpair,balance4,balance1,anti4", diag_ok},
 #endif
 };
 
