@@ -290,7 +290,6 @@ std::vector<int> balance_tile(const int32_t *csp, const int32_t *csn, const int3
             return (int)(rng % (uint64_t)m);
         };
         const int iters = 40 * units * waves;
-        std::vector<int64_t> others(steps);
         for (int it = 0; it < iters; it++) {
             const int a = rnd(waves), b0 = rnd(waves - 1), b = b0 >= a ? b0 + 1 : b0;
             const int i = rnd(upw), j = rnd(upw);
