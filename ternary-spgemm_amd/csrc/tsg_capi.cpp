@@ -48,6 +48,7 @@ struct tsg_tcsc {
     struct JitVariant {
         int nw = 0, waves = 0, Npad = 0;
         int piece_rows = 0;               // 64-row image: rows per DMA piece (its X^T layout; 0 = row layout)
+        bool pair = false;                // 64-row 4-wave streams run by 8-wave workgroups of wave pairs
         int nch = 0, chunk = 0;           // X^T chunks of the image and K rows per chunk
         tsg::JitModule mod;               // dispatcher + generated code, loaded
         uint32_t *d_wcode = nullptr;      // per (column tile, stream): byte offset of its code
@@ -706,7 +707,11 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
         }
 #endif
     DeviceGuard g(h->device);
-    const std::string err = v.mod.load(img.code, nw, waves, r64, half);
+    // the 64-row image's 4-wave streams: run by 8-wave workgroups of
+    // half-masked wave pairs (TSG_JIT_PAIR=1, read at load: A/B)
+    const char *pv = tsg::knob_value("TSG_JIT_PAIR");
+    const bool pair = r64 && waves == 4 && !half && pv && pv[0] == '1';
+    const std::string err = v.mod.load(img.code, nw, waves, r64, half, pair);
     if (!err.empty()) return fail(TSG_ERR_HIP, "jit kernel (width " + std::to_string(nw) + "): " + err);
     const size_t wb = img.wcode.size() * sizeof(uint32_t);
     if (hipMalloc(&v.d_wcode, std::max<size_t>(wb, 4)) != hipSuccess) {
@@ -751,6 +756,7 @@ int ensure_jit_variant(tsg_tcsc *h, int nw, int waves = tsg::kJitWaves, hipStrea
     }
     v.nw = nw;
     v.waves = waves;
+    v.pair = pair;
     v.Npad = img.Npad;
     v.piece_rows = img.piece_rows;
     v.nch = img.nch;
@@ -1059,7 +1065,8 @@ int run_dev(tsg_tcsc *h, const float *dX, const float *db, const float *dalpha, 
     const int lrc = h->kind == tsg_tcsc::kJit
         ? tsg::launch_tcsc_jit(jv->mod, direct ? dX : h->d_work, Mp, jv->d_wcode, db, dalpha, dY, M, N, jv->Npad,
                                jv->nch, prelu ? 1 : 0, h->d_status, jv->nw * jv->waves,
-                               jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0, lastadj, xtouch, tnear)
+                               jv->pair ? 2 * jv->waves : jv->waves, gn, gm, tmask, s, tile_m, direct ? K : 0,
+                               lastadj, xtouch, tnear)
         : tsg::launch_tcsc_rx(h->d_work, Mp, h->d_seg, h->d_ent, db, dalpha, dY, M, N, h->rimg.Npad,
                               h->rimg.nch, prelu ? 1 : 0, s);
     if (lrc != 0)

@@ -210,8 +210,10 @@ struct JitModule {
     void *module = nullptr;        // hipModule_t
     void *function = nullptr;      // hipFunction_t of tsg_jit_kernel
     void *probe = nullptr;         // hipFunction_t of tsg_jit_probe (region check, at load)
+    // pair: the 64-row image's 4-wave streams run by 8-wave workgroups of
+    // half-masked wave pairs (lib/tsg_jit64p_w<nw>.co; launch 8 waves)
     std::string load(const std::vector<uint32_t> &code, int nw = kJitNW, int waves = kJitWaves,
-                     bool rows64 = false, bool half = false);  // "" on success
+                     bool rows64 = false, bool half = false, bool pair = false);  // "" on success
     void unload();
 };
 // xrow > 0: the 64-row image stages straight from X (xrow floats per row);

@@ -919,10 +919,12 @@ namespace {
 // tsg_jit_w<nw>.co (same kernel built with TSG_JIT_NW=nw, Makefile); 4-wave
 // workgroups: tsg_jit_w<nw>_4w.co (TSG_JIT_WAVES=4); the 64-row image:
 // tsg_jit64_w<nw>[_4w].co (TSG_JIT_ROWS64=1), its half ring
-// tsg_jit64h_w<nw>.co (4 waves, TSG_JIT_HALF=1).
-std::string template_name(int nw, int waves, bool r64, bool half)
+// tsg_jit64h_w<nw>.co (4 waves, TSG_JIT_HALF=1), its wave pairs
+// tsg_jit64p_w<nw>.co (4-wave streams, TSG_JIT_PAIR=1).
+std::string template_name(int nw, int waves, bool r64, bool half, bool pair)
 {
     return r64 && half ? "tsg_jit64h_w" + std::to_string(nw) + ".co"
+           : r64 && pair ? "tsg_jit64p_w" + std::to_string(nw) + ".co"
            : r64 ? "tsg_jit64_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co"
            : nw == kJitNW && waves == kJitWaves ? "tsg_jit.co"
            : "tsg_jit_w" + std::to_string(nw) + (waves == kJitWaves ? "" : "_4w") + ".co";
@@ -947,9 +949,9 @@ namespace {
 // objects missing exercises the fallbacks), else the copy embedded in the
 // library, else the file next to the library (a build without the table
 // entry).
-std::string read_template(int nw, int waves, bool r64, bool half, std::vector<unsigned char> &img)
+std::string read_template(int nw, int waves, bool r64, bool half, bool pair, std::vector<unsigned char> &img)
 {
-    const std::string name = template_name(nw, waves, r64, half);
+    const std::string name = template_name(nw, waves, r64, half, pair);
     std::string path;
     if (const char *dir = knob_value("TSG_JIT_DIR")) {
         path = std::string(dir) + "/" + name;
@@ -975,10 +977,10 @@ std::string read_template(int nw, int waves, bool r64, bool half, std::vector<un
 
 }  // namespace
 
-std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves, bool r64, bool half)
+std::string JitModule::load(const std::vector<uint32_t> &code, int nw, int waves, bool r64, bool half, bool pair)
 {
     std::vector<unsigned char> img;
-    const std::string rerr = read_template(nw, waves, r64, half, img);
+    const std::string rerr = read_template(nw, waves, r64, half, pair, img);
     if (!rerr.empty()) return rerr;
     if (img.size() < sizeof(Elf64_Ehdr)) return "jit template too small";
     Elf64_Ehdr eh;

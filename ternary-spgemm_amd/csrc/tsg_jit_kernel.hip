@@ -73,16 +73,30 @@ namespace {
 #ifndef TSG_JIT_HALF
 #define TSG_JIT_HALF 0
 #endif
+// TSG_JIT_PAIR=1 (64-row image, 4-wave streams; lib/tsg_jit64p_w<NW>.co): an
+// 8-wave workgroup runs the 4-wave image -- waves w and w + 4 (one SIMD) run
+// stream w, each on one half of the tile's rows (exec = lanes 0-31, resp.
+// 32-63).  A lone wave per SIMD issues a VOP2 only every ~5.5 cycles; two
+// half-masked waves keep the SIMD issuing.  Together the pair stages the
+// stream's 12 DMA pieces (each wave its lanes' halves: the LDS-DMA address is
+// per lane), reads and touches what the 4-wave wave would; each wave stores
+// its half of the rows.
+#ifndef TSG_JIT_PAIR
+#define TSG_JIT_PAIR 0
+#endif
 constexpr int kJWaves = TSG_JIT_WAVES;
 constexpr int kJNW = TSG_JIT_NW;
 constexpr bool kJRows64 = TSG_JIT_ROWS64 != 0;
 constexpr bool kJHalf = TSG_JIT_HALF != 0;
+constexpr bool kJPair = TSG_JIT_PAIR != 0;
 static_assert(!kJHalf || (kJRows64 && TSG_JIT_WAVES == 4), "the half ring is a 4-wave 64-row image");
+static_assert(!kJPair || (kJRows64 && TSG_JIT_WAVES == 4 && !kJHalf), "wave pairs run the 4-wave 64-row image");
 static_assert(kJNW == 64 || kJNW == 32 || kJNW == 16 || kJNW == 8 || (kJRows64 && kJNW == 128), "stream width");
 static_assert(kJWaves == 8 || (kJWaves == 4 && kJNW < 64), "waves per workgroup");
 constexpr int kJTileM = kJRows64 ? 64 : 128;
 constexpr int kJRowsPerLane = kJTileM / 64;
 constexpr int kJTileCols = kJWaves * kJNW;
+constexpr int kJThreads = (kJPair ? 2 : 1) * kJWaves * 64;  // workgroup size (wave pairs: 8 waves, 4 streams)
 constexpr int kJRing = 3;                            // LDS buffers in the X^T ring (tsg_internal.h)
 constexpr int kJChunk = kJRows64 ? (kJHalf ? 96 : 192) : 96;  // K rows per chunk = 48 (half ring 24) quads / pairs
 constexpr int kJUnits = kJRows64 ? kJChunk / 4 : kJChunk / 2;  // 1-KiB LDS units per chunk
@@ -157,7 +171,7 @@ extern "C" __global__ __launch_bounds__(64) void tsg_jit_probe(uint32_t *__restr
 }
 
 // (the half ring: two workgroups per CU, so at most 256 VGPRs -- two waves per SIMD)
-extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_JIT_KERNEL_NAME(
+extern "C" __global__ __launch_bounds__(kJThreads, kJHalf ? 2 : 1) void TSG_JIT_KERNEL_NAME(
     const float *__restrict__ XT, int Mp, const uint32_t *__restrict__ wcode,
     const float *__restrict__ b, const float *__restrict__ alpha, float *__restrict__ Y, int M, int N,
     int nch, int mtiles, int ntiles, int prelu, uint32_t *__restrict__ status, int gn, int gm,
@@ -168,7 +182,11 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     // LDS is only addressed from the generated code, at absolute offsets from
     // 0 (the only LDS object): this use keeps the allocation in the descriptor
     asm volatile("; lds %0" ::"v"(lds));
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the wave's stream index (wave pairs: waves w and w + 4 share stream w)
+    // and, for a pair, which half of the rows it runs
+    const int wraw = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wave = kJPair ? (wraw & 3) : wraw;
+    const int rhalf = kJPair ? (wraw >> 2) : 0;
 
     // Base of the generated region: s_getpc + a literal that the loader-side
     // patcher (tsg_jit.cpp) sets to (region vaddr - vaddr of the s_add).
@@ -271,17 +289,33 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
     // row layout, direct X: the last chunk starts lastadj bytes below its slot (K - 188)
     const uint32_t adj = direct ? (uint32_t)lastadj : 0u;
 
+#if TSG_JIT_PAIR
+    // wave pairs: the stream runs with exec = the wave's half of the lanes;
+    // exec is saved around it (the dispatcher itself runs on all 64 lanes)
+    const uint64_t emask = rhalf ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+    uint64_t esave;
+#define TSG_JIT_EXEC_IN "s_mov_b64 %[es], exec\n\ts_mov_b64 exec, %[em]\n\t"
+#define TSG_JIT_EXEC_OUT "\n\ts_mov_b64 exec, %[es]"
+#define TSG_JIT_EXEC_OPS , [es] "=&s"(esave)
+#define TSG_JIT_EXEC_INS , [em] "s"(emask)
+#else
+#define TSG_JIT_EXEC_IN ""
+#define TSG_JIT_EXEC_OUT ""
+#define TSG_JIT_EXEC_OPS
+#define TSG_JIT_EXEC_INS
+#endif
 #define TSG_JIT_CALL(...)                                                                           \
-    asm volatile("s_getpc_b64 s[94:95]\n"                                                           \
+    asm volatile(TSG_JIT_EXEC_IN                                                                    \
+                 "s_getpc_b64 s[94:95]\n"                                                           \
                  ".Ljr%=:\n\t"                                                                      \
                  "s_add_u32 s94, s94, (.Ljb%= - .Ljr%=)\n\t"                                        \
                  "s_addc_u32 s95, s95, 0\n\t"                                                       \
                  "s_setpc_b64 %[cp]\n"                                                              \
-                 ".Ljb%=:"                                                                          \
-                 : __VA_ARGS__                                                                      \
+                 ".Ljb%=:" TSG_JIT_EXEC_OUT                                                         \
+                 : __VA_ARGS__ TSG_JIT_EXEC_OPS                                                     \
                  : [cp] "s"(cp), "{s[92:93]}"(base), "{s[90:91]}"(tbase), "{s[80:81]}"(xbase), "{s82}"(stride),  \
                    "{s83}"(wb), "{s87}"(adj),                                                          \
-                   TSG_JIT_IN                                                                       \
+                   TSG_JIT_IN TSG_JIT_EXEC_INS                                                      \
                  : TSG_JIT_CLOBBERS)
 #if TSG_JIT_ROWS64  // one accumulator VGPR per column (acc0 = v116; 4 waves: v122, half ring v116)
 #if TSG_JIT_WAVES == 8 || TSG_JIT_HALF
@@ -350,6 +384,7 @@ extern "C" __global__ __launch_bounds__(kJWaves * 64, kJHalf ? 2 : 1) void TSG_J
 #undef TSG_JIT_CALL
 
     if (ncol0 >= N) return;
+    if (kJPair && (lane >> 5) != rhalf) return;  // the pair's other wave holds these rows
 #pragma unroll
     for (int r = 0; r < kJRowsPerLane; r++) {
         const int m = m0 + kJRowsPerLane * lane + r;

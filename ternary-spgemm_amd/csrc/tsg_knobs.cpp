@@ -118,6 +118,7 @@ const Knob kKnobs[] = {
     {"TSG_JIT_FAR", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_XDIRECT", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_HALF", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
+    {"TSG_JIT_PAIR", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_QBLOCK", "16 | 8", [](const char *v) { return one_of(v, {"16", "8"}); }},
     {"TSG_JIT_STAGGER", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},
     {"TSG_JIT_PRIO", "0 | 1", [](const char *v) { return one_of(v, {"0", "1"}); }},

@@ -191,3 +191,35 @@ def test_rows64_half_ring(tsg, oracle_mod, monkeypatch, M, K, N):
         torch.cuda.synchronize()
         assert _bits_eq(Y.cpu().numpy(), ref), (M, K, N, direct, h.jit_width(M), h.jit_waves(M))
     h.close()
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 4096, 16384), (37, 1000, 4096), (1, 777, 2048), (130, 1000, 2048),
+                                   (64, 96, 1500), (70, 97, 3000), (1024, 4096, 1024)])
+def test_rows64_wave_pairs(tsg, oracle_mod, monkeypatch, M, K, N):
+    """Wave pairs (TSG_JIT_PAIR=1: the 4-wave streams run by 8-wave
+    workgroups, waves w and w + 4 on one half of the rows each, exec-masked;
+    tsg_jit_kernel.hip): staged and direct X, with PReLU, bit for bit against
+    the oracle -- every row is stored by exactly one wave of its pair and
+    every DMA piece is staged by the two halves together."""
+    import torch
+    O = oracle_mod
+    t = O.tcsc_encode(O.gen_ternary(K, N, 4, M + K + N + 5))
+    b = np.linspace(-2, 2, N).astype(np.float32)
+    alpha = np.linspace(0.05, 0.3, N).astype(np.float32)
+    Xh = O.init_x_frac(M, K, 29)
+    ref = O.base_tcsc(Xh, t, b)
+    ref_p = O.base_tcsc_prelu(Xh, t, b, alpha)
+    monkeypatch.setenv("TSG_JIT_PAIR", "1")
+    h = _handle(tsg, t, K, N)
+    assert h.jit_waves(M) == 4, (M, K, N, h.jit_width(M))  # these shapes pick 4-wave streams
+    X = torch.from_numpy(Xh).cuda()
+    bt = torch.from_numpy(b).cuda()
+    at = torch.from_numpy(alpha).cuda()
+    for direct in ("0", "1"):
+        monkeypatch.setenv("TSG_JIT_XDIRECT", direct)
+        Y = h.gemm_torch(X, bt)
+        Yp = h.gemm_torch(X, bt, alpha=at)
+        torch.cuda.synchronize()
+        assert _bits_eq(Y.cpu().numpy(), ref), (M, K, N, direct, h.jit_width(M))
+        assert _bits_eq(Yp.cpu().numpy(), ref_p), (M, K, N, direct, h.jit_width(M))
+    h.close()

@@ -179,6 +179,7 @@ def _small_tcsc(oracle_mod):
     ("TSG_KERNEL", "fast", "expected"),
     ("TSG_ELL_VARIANT", "7", "expected"),
     ("TSG_JIT_HALF", "2", "expected"),
+    ("TSG_JIT_PAIR", "2", "expected"),
     ("TSG_JIT_XDIRECT", "on", "expected"),
     ("TSG_JIT_QBLOCK", "4", "expected"),
     ("TSG_ELL_COPIES", "3", "expected"),
@@ -245,7 +246,8 @@ def test_code_objects_embedded(tsg):
     expected = (["tsg_jit.co"] + [f"tsg_jit_w{w}.co" for w in (32, 16, 8)]
                 + [f"tsg_jit_w{w}_4w.co" for w in (32, 16, 8)]
                 + [f"tsg_jit64_w{w}.co" for w in (128, 64, 32, 16, 8)]
-                + [f"tsg_jit64_w{w}_4w.co" for w in (32, 16, 8)] + [f"tsg_jit64h_w{w}.co" for w in (32, 16, 8)])
+                + [f"tsg_jit64_w{w}_4w.co" for w in (32, 16, 8)] + [f"tsg_jit64h_w{w}.co" for w in (32, 16, 8)]
+                + [f"tsg_jit64p_w{w}.co" for w in (32, 16, 8)])
     assert sorted(got) == sorted(expected) == on_disk
     for name, blob in got.items():
         with open(os.path.join(libdir, name), "rb") as f:
