@@ -634,15 +634,17 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // than 12,12, profiles/r02_jit_knobs_ab.txt); TSG_JIT_READS="G,RA" overrides.
     int G = std::max(1, S / 3), RA = S - std::max(1, S / 3);
     // 64-row image, narrow streams (<= 32 columns) or sparse W (density <=
-    // 1/8): groups of 5, read-ahead 19 -- shorter groups between the waits
-    // where a group feeds few adds (round 6, kernel us, alternating,
-    // profiles/r06z_reads_ab.jsonl, r06z2_reads_ab.jsonl: configs[1] 61.3-61.4
-    // -> 60.1-60.2, s = 16 432-435 -> 425-427, s = 8 667 -> 662); the wide
-    // dense streams keep 8,16 (configs[2] 6,18 and 7,17 +7%, 5,19 even:
-    // there the group count moves the per-group code touches)
+    // 1/8): groups of 5, read-ahead 19, and of 3 (read-ahead 21) for streams
+    // of <= 16 columns -- shorter groups between the waits where a group
+    // feeds few adds (round 6, kernel us, alternating, profiles/
+    // r06z3_reads_rule_ab.jsonl, r06z5_reads3_ab.jsonl: configs[1] 61.6 ->
+    // 60.0 -> 58.1, (1024, 4096, 1024) 56.0 -> 55.0, M = 192 96.4 -> 92.2,
+    // s = 16 431.7 -> 424.5, s = 8 664.0 -> 658.3); the wide dense streams
+    // keep 8,16 (configs[2] 6,18 and 7,17 +7%, 5,19 even: there the group
+    // count moves the per-group code touches, r06z_reads_ab.jsonl)
     if (r64 && !B && (nw <= 32 || density <= 0.125)) {
-        G = 5;
-        RA = S - 5;
+        G = nw <= 16 ? 3 : 5;
+        RA = S - G;
     }
     if (const char *rv = knob_value("TSG_JIT_READS")) std::sscanf(rv, "%d,%d", &G, &RA);
     if (G < 1 || RA < 0 || G + RA > S) {
