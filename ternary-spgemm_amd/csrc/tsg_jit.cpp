@@ -641,8 +641,10 @@ void build_jit_code(const int32_t *csp, const int32_t *csn, const int32_t *rip, 
     // 60.0 -> 58.1, (1024, 4096, 1024) 56.0 -> 55.0, M = 192 96.4 -> 92.2,
     // s = 16 431.7 -> 424.5, s = 8 664.0 -> 658.3); the wide dense streams
     // keep 8,16 (configs[2] 6,18 and 7,17 +7%, 5,19 even: there the group
-    // count moves the per-group code touches, r06z_reads_ab.jsonl)
-    if (r64 && !B && (nw <= 32 || density <= 0.125)) {
+    // count moves the per-group code touches, r06z_reads_ab.jsonl), and so
+    // do 32-wide streams of dense W (s = 2: (192, 4096, 16384) 162.7 vs 170.9
+    // with 5, r06z7_reads_dense_ab.jsonl)
+    if (r64 && !B && (nw <= 16 || (nw <= 32 && density <= 0.375) || density <= 0.125)) {
         G = nw <= 16 ? 3 : 5;
         RA = S - G;
     }
